@@ -1,0 +1,169 @@
+"""Engine interface and the device-resident client store.
+
+An *engine* owns the clients hosted by one rank (one GPU): their datasets,
+parameters and optimiser state, all resident on the device in
+structure-of-arrays form, and exposes the compute primitives the federated
+protocol needs:
+
+* ``train``          – local training of a set of clients (reference
+  ``ClientTrainer.run``, `src/Trainer/client_trainer.py:360-419`);
+* ``forward_rows``   – per-row squared reconstruction error and/or latents of
+  (parameter-vector, dataset) pairs: vote scores, FedMSE weights,
+  verification, AE anomaly scores, SAE latents
+  (`src/Trainer/client_trainer.py:208-247`, `:115-130`,
+  `src/Trainer/model_verifier.py:86-99`, `src/Evaluator/evaluator.py:52-94`);
+* ``weighted_sum``   – FedAvg / MSEAvg reduction (`client_trainer.py:107-134`);
+* ``param_drift``    – verifier drift, sum of per-tensor L2 norms
+  (`src/Trainer/model_verifier.py:79-84`);
+* ``cen_scores`` + ``auc`` – SAE-CEN scoring and ROC-AUC
+  (`src/Model/Centroid.py:15-35`, `src/Evaluator/evaluator.py:21-28`).
+
+Two implementations: ``TorchEngine`` (pure PyTorch, reference-exact math,
+runs anywhere) and ``HipEngine`` (hand-written gfx950 kernels).  The HIP
+engine never falls back to torch for these primitives: if its library is
+missing it raises.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..models.layout import DP, P_PAD, ModelDims, DEFAULT_DIMS, canonical_to_padded, padded_to_canonical
+
+
+@dataclass
+class TrainHParams:
+    epochs: int
+    batch_size: int = 12
+    lr: float = 1e-3
+    shrink_lambda: float = 0.0      # 0 for the plain AE
+    fedprox_mu: float = 0.0         # 0 unless update_type == "fedprox"
+    patience: int = 1
+    beta1: float = 0.9
+    beta2: float = 0.999
+    eps: float = 1e-8
+
+
+@dataclass
+class TrainResult:
+    local_ids: List[int]
+    epochs_run: np.ndarray               # int [k]
+    tracking: List[List[Tuple[float, float]]]  # per client: [(train_loss, valid_loss)] per epoch
+    best_epoch: np.ndarray               # int [k] (-1 if never improved)
+
+
+def pad_features(x: np.ndarray) -> np.ndarray:
+    """[n, D] -> [n, DP] float32, zero padded (aligned 512-byte rows)."""
+    n, d = x.shape
+    out = np.zeros((n, DP), dtype=np.float32)
+    out[:, :d] = x
+    return out
+
+
+class ClientStore:
+    """Structure-of-arrays state of the clients hosted by this rank.
+
+    Parameters use the padded layout (``models/layout.py``).  Sized once per
+    combination: ~37 KB x 5 state vectors per client plus its data
+    (~2.2 MB per N-BaIoT client) — trivially resident in 288 GB of HBM.
+    """
+
+    def __init__(self, num_clients: int, device: torch.device):
+        C = num_clients
+        f32 = dict(dtype=torch.float32, device=device)
+        self.num_clients = C
+        self.device = device
+        self.params = torch.zeros(C, P_PAD, **f32)
+        self.adam_m = torch.zeros(C, P_PAD, **f32)
+        self.adam_v = torch.zeros(C, P_PAD, **f32)
+        self.adam_step = torch.zeros(C, dtype=torch.int32, device=device)
+        self.anchor = torch.zeros(C, P_PAD, **f32)
+        self.best = torch.zeros(C, P_PAD, **f32)
+        # data: concatenated, row-padded to DP columns
+        self.train = self.valid = self.test = None
+        self.train_off = self.valid_off = self.test_off = None
+        self.test_label = None
+
+    @staticmethod
+    def _concat(arrays: Sequence[np.ndarray], device):
+        offs = np.zeros(len(arrays) + 1, dtype=np.int64)
+        for i, a in enumerate(arrays):
+            offs[i + 1] = offs[i] + a.shape[0]
+        buf = np.concatenate([pad_features(a) for a in arrays], 0) if arrays else np.zeros((0, DP), np.float32)
+        return torch.from_numpy(buf).to(device), offs
+
+    def load_data(self, train: Sequence[np.ndarray], valid: Sequence[np.ndarray],
+                  test: Sequence[np.ndarray], test_label: Sequence[np.ndarray]):
+        self.train, self.train_off = self._concat(train, self.device)
+        self.valid, self.valid_off = self._concat(valid, self.device)
+        self.test, self.test_off = self._concat(test, self.device)
+        lab = np.concatenate([np.asarray(l, dtype=np.int32) for l in test_label]) if test_label else np.zeros(0, np.int32)
+        self.test_label = torch.from_numpy(lab).to(self.device)
+        self.test_label_np = lab
+
+    def rows(self, split: str, c: int) -> torch.Tensor:
+        buf = getattr(self, split)
+        off = getattr(self, split + "_off")
+        return buf[int(off[c]):int(off[c + 1])]
+
+    def labels(self, c: int) -> np.ndarray:
+        return self.test_label_np[int(self.test_off[c]):int(self.test_off[c + 1])]
+
+
+class Engine:
+    name = "abstract"
+
+    def __init__(self, dims: ModelDims = DEFAULT_DIMS, device: Optional[torch.device] = None):
+        self.dims = dims
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.store: Optional[ClientStore] = None
+
+    # -- setup -----------------------------------------------------------------
+    def setup(self, train, valid, test, test_label, init_canonical: torch.Tensor):
+        C = len(train)
+        self.store = ClientStore(C, self.device)
+        self.store.load_data(train, valid, test, test_label)
+        p = canonical_to_padded(init_canonical.to(torch.float32), self.dims).to(self.device)
+        self.store.params.copy_(p)
+        self.store.anchor.copy_(p)  # FedProx anchor starts at the init weights (Q11)
+        self.store.best.copy_(p)
+
+    def to_device(self, x: np.ndarray) -> torch.Tensor:
+        return torch.from_numpy(pad_features(np.asarray(x, dtype=np.float32))).to(self.device)
+
+    def canonical(self, padded: torch.Tensor) -> torch.Tensor:
+        return padded_to_canonical(padded, self.dims)
+
+    # -- primitives (implemented by subclasses) --------------------------------
+    def train(self, local_ids: Sequence[int], hp: TrainHParams) -> TrainResult:
+        raise NotImplementedError
+
+    def forward_rows(self, params: torch.Tensor, items: Sequence[Tuple[int, torch.Tensor]],
+                     want_sse: bool = True, want_latent: bool = False):
+        """For each (param_row, data[n, DP]) item: per-row SSE over the real
+        D columns and/or latents [n, Z].  Returns (sse_list, latent_list)."""
+        raise NotImplementedError
+
+    def weighted_sum(self, stack: torch.Tensor, weights: Sequence[float]) -> torch.Tensor:
+        raise NotImplementedError
+
+    def param_drift(self, hist: torch.Tensor, new: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def cen_scores(self, train_lat: Sequence[torch.Tensor], test_lat: Sequence[torch.Tensor]) -> List[torch.Tensor]:
+        raise NotImplementedError
+
+    def auc(self, scores: Sequence[torch.Tensor], labels: Sequence[torch.Tensor]) -> np.ndarray:
+        raise NotImplementedError
+
+    def standardize_ddof1(self, x: torch.Tensor) -> torch.Tensor:
+        """(x - mean) / (std_ddof1 + 1e-8) over the real D columns
+        (`src/Trainer/client_trainer.py:220-223`)."""
+        raise NotImplementedError
+
+    def synchronize(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)

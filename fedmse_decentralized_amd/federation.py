@@ -1,0 +1,488 @@
+"""The decentralised federated round loop (one sweep combination).
+
+Reference: the body of the combination loop in `src/main.py:108-379`
+(client construction, per-round select -> train -> vote -> aggregate ->
+broadcast -> verify -> evaluate -> report -> early stop).
+
+MI355X design:
+
+* every rank (one process per GPU) hosts a contiguous shard of the clients
+  in an engine (device-resident data + SoA client state);
+* protocol *decisions* (selection, election, aggregation plan, early stop)
+  are a replicated state machine: every rank computes them from identical
+  inputs, so no decision ever needs to be broadcast;
+* the logical peer messages are three tiny collectives per round
+  (score all-reduce, parameter all-gather, metric all-reduce) over RCCL;
+* all selected clients of a rank train concurrently in one fused kernel
+  launch; evaluation of all hosted clients is a few batched launches.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import random
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .config import ExperimentConfig, load_device_list
+from .data.csv import load_data
+from .data.prepare import ClientData, prepare_federation
+from .data.synthetic import ClientRaw, SyntheticSpec, generate_client
+from .engine import Engine, TrainHParams, make_engine
+from .eval.evaluator import evaluate_clients
+from .io import checkpoint as ckpt
+from .io import reports
+from .models.layout import P_PAD, ModelDims
+from .models.reference import init_client_params
+from .parallel.comm import Comm, LoopbackComm
+from .parallel.sharding import ShardMap
+from .protocol.aggregation import make_plan
+from .protocol.early_stop import GlobalEarlyStop
+from .protocol.election import elect_aggregator, select_clients
+from .protocol.verification import Verifier, VerifierState
+from .utils.rng_replay import HostNoise, TorchRngReplay
+from .utils.telemetry import Telemetry
+
+log = logging.getLogger("fedmx")
+
+_PREP_CACHE: Dict[tuple, Tuple[List[ClientData], np.ndarray]] = {}
+
+
+# ----------------------------------------------------------------------------
+# data
+# ----------------------------------------------------------------------------
+
+def load_federation_data(cfg: ExperimentConfig, py_rng: random.Random) -> Tuple[List[ClientData], np.ndarray]:
+    """Device sampling + per-client preparation with the reference RNG order.
+
+    Consumes ``py_rng`` exactly like `src/main.py:126` (``random.sample`` of
+    the device list); the numpy RNG is a private ``RandomState(data_seed)``.
+    Prepared data is cached per process (identical for every combination).
+    """
+    if cfg.synthetic:
+        spec = SyntheticSpec(kind=cfg.synthetic, n_clients=cfg.network_size, iid=cfg.synthetic_iid,
+                             alpha=cfg.synthetic_alpha, seed=cfg.synthetic_seed)
+        entries = list(range(cfg.network_size))
+        chosen = py_rng.sample(entries, cfg.network_size)
+        key = ("synthetic", cfg.synthetic, cfg.network_size, cfg.synthetic_iid, cfg.synthetic_alpha,
+               cfg.synthetic_seed, cfg.data_seed, cfg.new_device, cfg.scaler, tuple(chosen))
+        if key not in _PREP_CACHE:
+            raws = [generate_client(spec, i) for i in chosen]
+            _PREP_CACHE[key] = prepare_federation(raws, cfg.data_seed, cfg.new_device, cfg.scaler)
+        return _PREP_CACHE[key]
+    dl = load_device_list(cfg.config_file)
+    if len(dl.devices_list) < cfg.network_size:
+        raise ValueError(f"{cfg.config_file} lists {len(dl.devices_list)} devices < network_size {cfg.network_size}")
+    chosen = py_rng.sample(dl.devices_list, cfg.network_size)
+    key = ("csv", os.path.abspath(cfg.config_file), cfg.network_size, cfg.data_seed, cfg.new_device, cfg.scaler,
+           tuple(d.name for d in chosen))
+    if key not in _PREP_CACHE:
+        raws = []
+        for d in chosen:
+            log.info("Loading data from {}...".format(d.name))
+            normal = load_data(dl.resolve(d.normal_data_path))
+            abnormal = load_data(dl.resolve(d.abnormal_data_path))
+            if cfg.new_device:
+                if not d.test_normal_data_path:
+                    raise ValueError(f"device {d.name} has no test_normal_data_path (needed with new_device)")
+                tn = load_data(dl.resolve(d.test_normal_data_path))
+            else:
+                tn = np.zeros((0, normal.shape[1]))
+            log.info(f"{d.name} has {len(normal)} normal data and {len(abnormal)} abnormal data")
+            raws.append(ClientRaw(d.name, normal, abnormal, tn))
+        _PREP_CACHE[key] = prepare_federation(raws, cfg.data_seed, cfg.new_device, cfg.scaler)
+    return _PREP_CACHE[key]
+
+
+# ----------------------------------------------------------------------------
+# federation
+# ----------------------------------------------------------------------------
+
+@dataclass
+class RoundResult:
+    round: int
+    selected: List[int]
+    aggregator: Optional[int]
+    metrics: np.ndarray
+    verification: List[Dict]
+    epochs_run: Dict[int, int]
+    stop: bool = False
+    times_ms: Dict[str, float] = field(default_factory=dict)
+
+
+class Federation:
+    def __init__(self, cfg: ExperimentConfig, model_type: str, update_type: str, run: int,
+                 comm: Optional[Comm] = None, device: Optional[torch.device] = None,
+                 early_stop: Optional[GlobalEarlyStop] = None, engine: Optional[Engine] = None,
+                 telemetry: Optional[Telemetry] = None, write_reports: bool = True):
+        self.cfg = cfg
+        self.model_type = model_type
+        self.update_type = update_type
+        self.run = run
+        self.comm = comm or LoopbackComm(device)
+        self.device = torch.device(device) if device is not None else self.comm.device
+        self.dims = ModelDims(cfg.dim_features, cfg.hidden_neus, cfg.latent_dim)
+        self.early = early_stop or GlobalEarlyStop(cfg.global_patience, cfg.compat)
+        self.engine = engine or make_engine(cfg.backend, self.dims, self.device)
+        self.tel = telemetry or Telemetry(cfg.trace_file, sync_fn=self.engine.synchronize, rank=self.comm.rank)
+        self.write_reports = write_reports and self.comm.is_root
+        self.round_idx = 0
+        self.last_metrics: Optional[np.ndarray] = None
+        self.latent_log: Dict[int, Dict[str, Tuple[np.ndarray, np.ndarray]]] = {}
+
+    # -- setup -------------------------------------------------------------------
+    def setup(self):
+        cfg = self.cfg
+        # set_seeds(run*10000) then random/np re-seeded with data_seed (src/main.py:115-117)
+        self.py_rng = random.Random(cfg.data_seed)
+        clients, dev = load_federation_data(cfg, self.py_rng)
+        self.clients = clients
+        N = len(clients)
+        self.N = N
+        self.shard = ShardMap(N, self.comm.world_size)
+        self.local = self.shard.local_ids(self.comm.rank)
+        init, rng_state = init_client_params(N, self.run * 10000, self.dims)
+        self.noise = TorchRngReplay(rng_state, self.dims) if cfg.compat == "reference" else HostNoise(self.run * 10000 + 17)
+        eng = self.engine
+        loc = [clients[c] for c in self.local]
+        eng.setup([c.train for c in loc], [c.valid for c in loc], [c.test for c in loc],
+                  [c.test_label for c in loc], init[self.local[0]:self.local[-1] + 1] if self.local else init[:0])
+        # replicated small tensors: every client's validation set (vote data) and the dev set
+        self.valid_all = [eng.to_device(c.valid) for c in clients]
+        self.dev_set = eng.to_device(dev)
+        self.agg_counts = [0] * N
+        self.verifier = Verifier(cfg.verification_threshold, cfg.performance_threshold,
+                                 cfg.verification_method, cfg.max_rejected_updates)
+        self.vstate: Dict[int, VerifierState] = {c: VerifierState() for c in self.local}
+        self.versions: Dict[int, torch.Tensor] = {}
+        self.last_received: List[Optional[int]] = [None] * N
+        self.hp = TrainHParams(
+            epochs=cfg.epoch, batch_size=cfg.batch_size, lr=cfg.lr_rate,
+            shrink_lambda=float(cfg.shrink_lambda) if self.model_type == "hybrid" else 0.0,
+            fedprox_mu=cfg.fedprox_mu if self.update_type == "fedprox" else 0.0,
+            patience=cfg.global_patience)
+        self.save_dirs = {c: cfg.client_save_dir(self.run, self.model_type, self.update_type, clients[c].name)
+                          for c in self.local}
+        if cfg.save_checkpoints:
+            for d in self.save_dirs.values():
+                os.makedirs(d, exist_ok=True)
+        if cfg.resume:
+            self.restore(ckpt.load_resume(self._resume_path(cfg.resume)))
+        return self
+
+    def _resume_path(self, base: str) -> str:
+        return base if self.comm.world_size == 1 else f"{base}.rank{self.comm.rank}"
+
+    # -- helpers -------------------------------------------------------------------
+    def _loc(self, cid: int) -> int:
+        return self.shard.to_local(self.comm.rank, cid)
+
+    def _mine(self, cid: int) -> bool:
+        s, e = self.shard.bounds(self.comm.rank)
+        return s <= cid < e
+
+    def _batch_mean_score(self, sse: torch.Tensor, bs: int) -> float:
+        """Mean over batches of per-batch MSE (`src/Trainer/client_trainer.py:226-241`)."""
+        D = self.dims.d_in
+        x = sse.detach().double().cpu().numpy()
+        n = x.shape[0]
+        tot, nb = 0.0, 0
+        for s in range(0, n, bs):
+            seg = x[s:s + bs]
+            tot += float(seg.sum() / (seg.shape[0] * D))
+            nb += 1
+        return tot / nb if nb else float("inf")
+
+    def _gather_params(self, sources: Sequence[int], selected: Sequence[int]) -> torch.Tensor:
+        """Stack [len(sources), P] of the given clients' params (all ranks)."""
+        st = self.engine.store
+        if self.comm.world_size == 1:
+            idx = torch.tensor([self._loc(c) for c in sources], dtype=torch.long, device=st.params.device)
+            return st.params.index_select(0, idx)
+        # slot layout: each rank packs its selected clients in selected order
+        per_rank: Dict[int, List[int]] = {}
+        for c in selected:
+            per_rank.setdefault(self.shard.owner(c), []).append(c)
+        slots = max(len(v) for v in per_rank.values())
+        mine = per_rank.get(self.comm.rank, [])
+        send = torch.zeros(slots, P_PAD, dtype=torch.float32, device=st.params.device)
+        if mine:
+            idx = torch.tensor([self._loc(c) for c in mine], dtype=torch.long, device=st.params.device)
+            send[:len(mine)] = st.params.index_select(0, idx)
+        allg = self.comm.all_gather(send)        # [world, slots, P]  (RCCL all-gather over xGMI)
+        rows = []
+        for c in sources:
+            r = self.shard.owner(c)
+            rows.append(allg[r, per_rank[r].index(c)])
+        return torch.stack(rows, 0)
+
+    # -- one round ---------------------------------------------------------------
+    def run_round(self) -> RoundResult:
+        cfg, eng, st = self.cfg, self.engine, self.engine.store
+        rnd = self.round_idx
+        N = self.N
+        D = self.dims.d_in
+        log.info(f"Starting round {rnd + 1}/{cfg.num_rounds}")
+
+        with self.tel.phase("select"):
+            selected = select_clients(self.py_rng, N, cfg.num_participants)
+            local_sel = [c for c in selected if self._mine(c)]
+
+        # ---------------- local training (all local selected clients, one launch)
+        with self.tel.phase("train"):
+            for c in local_sel:
+                log.info(f"Training client {c + 1}...")
+            res = eng.train([self._loc(c) for c in local_sel], self.hp) if local_sel else None
+            epochs_local = {}
+            if res is not None:
+                for i, c in enumerate(local_sel):
+                    epochs_local[c] = int(res.epochs_run[i])
+                    for e, (tl, vl) in enumerate(res.tracking[i]):
+                        log.info(f"[Client {c}] Epoch {e + 1} - Training loss: {tl} - Validating loss: {vl}")
+                    log.info(f"Client {c + 1} training done!")
+                if cfg.malicious_clients:
+                    for i, c in enumerate(local_sel):
+                        if c in cfg.malicious_clients:   # fault injection: poisoned update
+                            st.params[self._loc(c)].mul_(cfg.malicious_scale)
+
+        with self.tel.phase("io"):
+            if res is not None and cfg.save_checkpoints:
+                for i, c in enumerate(local_sel):
+                    if res.best_epoch[i] >= 0:
+                        ckpt.save_model_cpt(self.save_dirs[c], st.best[self._loc(c)], self.dims)
+                    ckpt.save_tracking(self.save_dirs[c], res.tracking[i])
+
+        # ---------------- vote scores (+ FedMSE dev MSE), one all-reduce
+        log.info("Starting voting for aggregator...")
+        with self.tel.phase("vote"):
+            vote_src = self.valid_all[selected[0]]
+            vs = eng.standardize_ddof1(vote_src)
+            items = [(self._loc(c), vs) for c in local_sel]
+            need_dev = self.update_type == "mse_avg"
+            if need_dev:
+                items += [(self._loc(c), self.dev_set) for c in local_sel]
+            sse, _ = eng.forward_rows(st.params, items, want_sse=True) if items else ([], None)
+            vec = torch.zeros(N, 3, dtype=torch.float64)
+            for i, c in enumerate(local_sel):
+                vec[c, 0] = self._batch_mean_score(sse[i], cfg.vote_batch_size)
+                if need_dev:
+                    s = sse[len(local_sel) + i]
+                    vec[c, 1] = float(s.double().sum().item()) / (s.shape[0] * D)
+                vec[c, 2] = epochs_local.get(c, 0)
+        with self.tel.phase("comm"):
+            vec = self.comm.all_reduce_sum(vec)
+        with self.tel.phase("vote"):
+            base_scores = {c: float(vec[c, 0]) for c in selected}
+            dev_mse = {c: float(vec[c, 1]) for c in selected}
+            epochs_all = {c: int(vec[c, 2]) for c in selected}
+            # torch-RNG replay: one iterator per train and per valid epoch loop
+            self.noise.iterators(2 * sum(epochs_all.values()))
+            el = elect_aggregator(selected, base_scores, self.agg_counts, cfg.max_aggregation, self.noise,
+                                  log_enabled=log.isEnabledFor(logging.INFO))
+            aggregator = el.aggregator
+
+        verification_results: List[Dict] = []
+        if aggregator is not None:
+            log.info(f"Client {aggregator + 1} selected as aggregator")
+            with self.tel.phase("aggregate"):
+                if self.update_type == "mse_avg":
+                    for _ in selected:          # calculate_mse_score per client (weights unused, Q3)
+                        self.noise.rand()
+                plan = make_plan(self.update_type, selected, aggregator, dev_mse, cfg.compat)
+            with self.tel.phase("comm"):
+                stack = self._gather_params([c for c, _ in plan], selected)
+            with self.tel.phase("aggregate"):
+                agg = eng.weighted_sum(stack, [w for _, w in plan])
+                self.agg_counts[aggregator] += 1
+                if self._mine(aggregator):
+                    st.params[self._loc(aggregator)].copy_(agg)
+                version = rnd
+                self.versions[version] = agg
+            with self.tel.phase("verify"):
+                verification_results = self._verify_all(agg, version, aggregator, rnd)
+            if self.write_reports:
+                with self.tel.phase("io"):
+                    log.info("Verification results for this round:")
+                    for r_ in verification_results:
+                        log.info(f"Client {r_['client_id']}: {'Verified' if r_['is_verified'] else 'Rejected'} "
+                                 f"(Rejected updates: {r_['rejected_updates']})")
+                    reports.append_verification(cfg, self.run, rnd, verification_results)
+        else:
+            log.warning("No aggregator selected for this round")
+
+        # ---------------- evaluation of every client
+        log.info("Calculating metrics for all models...")
+        with self.tel.phase("eval"):
+            er = evaluate_clients(eng, list(range(len(self.local))), self.model_type, cfg.metric,
+                                  keep_latents=cfg.save_latents)
+            vec = torch.zeros(N, dtype=torch.float64)
+            for i, c in enumerate(self.local):
+                vec[c] = float(er.metrics[i])
+        with self.tel.phase("comm"):
+            vec = self.comm.all_reduce_sum(vec)
+        metrics = vec.numpy().copy()
+        self.noise.iterators(N * (2 if self.model_type == "hybrid" else 1))
+        for i in range(N):
+            log.info(f"Client {i + 1} {cfg.metric} score: {metrics[i]}")
+        if cfg.save_latents and er.latents is not None:
+            names = [self.clients[c].name for c in self.local]
+            self.latent_log[rnd] = {n: l for n, l in zip(names, er.latents)}
+        with self.tel.phase("io"):
+            if self.write_reports:
+                reports.append_round_result(cfg, self.run, rnd, metrics, self.model_type, self.update_type)
+        self.last_metrics = metrics
+        stop = False
+        if cfg.global_early_stop:
+            stop = self.early.update(float(np.min(metrics)))
+        self.round_idx += 1
+        times = self.tel.end_round(round=rnd + 1, selected=len(selected), aggregator=aggregator)
+        return RoundResult(rnd, list(selected), aggregator, metrics, verification_results, epochs_all, stop, times)
+
+    def _verify_all(self, agg: torch.Tensor, version: int, aggregator: int, rnd: int) -> List[Dict]:
+        cfg, eng, st = self.cfg, self.engine, self.engine.store
+        N = self.N
+        D = self.dims.d_in
+        receivers = [c for c in self.local if c != aggregator]
+        # perf = 1 / (1 + MSE(V, model(V))) of the new aggregate (src/Trainer/model_verifier.py:86-99)
+        aggp = agg.unsqueeze(0)
+        if cfg.verification_method == "dev":
+            datasets = {c: ("dev", self.dev_set) for c in receivers}
+        elif cfg.compat == "reference":
+            # every client verifies on the last-constructed client's validation set (Q4)
+            datasets = {c: ("vlast", self.valid_all[N - 1]) for c in receivers}
+        else:
+            datasets = {c: (f"v{c}", self.valid_all[c]) for c in receivers}
+        keys = sorted({k for k, _ in datasets.values()})
+        keyed = {k: t for k, t in datasets.values()}
+        sse, _ = eng.forward_rows(aggp, [(0, keyed[k]) for k in keys], want_sse=True) if keys else ([], None)
+        perf = {}
+        for k, s in zip(keys, sse):
+            mse = float(s.double().sum().item()) / (s.shape[0] * D)
+            perf[k] = 1.0 / (1.0 + mse)
+        # drift against each receiver's previous received aggregate (grouped by version)
+        need = sorted({self.vstate[c].history_version for c in receivers if self.vstate[c].history_version is not None})
+        drift = {}
+        if need:
+            hist = torch.stack([self.versions[v] for v in need], 0)
+            d = eng.param_drift(hist, agg).double().cpu().numpy()
+            drift = {v: float(x) for v, x in zip(need, d)}
+        accept = []
+        vec = torch.zeros(N, 2, dtype=torch.float64)
+        for c in receivers:
+            vs_ = self.vstate[c]
+            dr = drift.get(vs_.history_version, 0.0) if vs_.history_version is not None else 0.0
+            dec = self.verifier.decide(c, vs_, version, perf[datasets[c][0]], dr, rnd)
+            self.verifier.apply(c, vs_, dec)
+            if dec.verified:
+                accept.append(c)
+            vec[c, 0] = vs_.rejected_updates
+            vec[c, 1] = 1.0
+        if accept:
+            idx = torch.tensor([self._loc(c) for c in accept], dtype=torch.long, device=st.params.device)
+            rows = agg.unsqueeze(0).expand(len(accept), -1)
+            st.params.index_copy_(0, idx, rows)
+            st.anchor.index_copy_(0, idx, rows)      # previous_global_model = deepcopy(model)
+        self.noise.model_inits(N - 1)                # verifier builds a fresh model per call (Q16)
+        # replicated bookkeeping: every non-aggregator received this version;
+        # drop aggregate versions no client references any more
+        for c in range(N):
+            if c != aggregator:
+                self.last_received[c] = version
+        live = {v for v in self.last_received if v is not None}
+        for v in list(self.versions):
+            if v not in live:
+                del self.versions[v]
+        vec = self.comm.all_reduce_sum(vec)
+        out = []
+        for c in range(N):
+            if c == aggregator:
+                continue
+            rej = int(vec[c, 0])
+            out.append({"client_id": c, "rejected_updates": rej, "is_verified": rej == 0})
+        return out
+
+    # -- whole combination -------------------------------------------------------
+    def run_all(self) -> float:
+        """Run ``num_rounds`` rounds (or until global early stop); returns the
+        combination's best metric (max over clients of the final models,
+        `src/main.py:367-374`)."""
+        cfg = self.cfg
+        while self.round_idx < cfg.num_rounds:
+            r = self.run_round()
+            if cfg.snapshot_every and self.round_idx % cfg.snapshot_every == 0:
+                self.save_snapshot()
+            if r.stop:
+                break
+        if self.last_metrics is None:
+            er = evaluate_clients(self.engine, list(range(len(self.local))), self.model_type, cfg.metric)
+            vec = torch.zeros(self.N, dtype=torch.float64)
+            for i, c in enumerate(self.local):
+                vec[c] = float(er.metrics[i])
+            self.last_metrics = self.comm.all_reduce_sum(vec).numpy()
+        if cfg.save_latents and self.latent_log:
+            parts = self.comm.all_gather_object(self.latent_log)
+            if self.comm.is_root:
+                merged: Dict[int, Dict] = {}
+                for p in parts:
+                    for r, d in p.items():
+                        merged.setdefault(r, {}).update(d)
+                path = os.path.join(cfg.output_root, f"Checkpoint/LatentData/{cfg.network_size}/{cfg.experiment_name}/"
+                                    f"Run_{self.run}/latent_{self.model_type}_{self.update_type}.pkl")
+                ckpt.save_latents(path, merged)
+        return float(np.max(self.last_metrics))
+
+    # -- resume ---------------------------------------------------------------------
+    def snapshot(self) -> Dict:
+        st = self.engine.store
+        vers = sorted(self.versions)
+        return {
+            "round_idx": self.round_idx,
+            "params": st.params.cpu(), "adam_m": st.adam_m.cpu(), "adam_v": st.adam_v.cpu(),
+            "adam_step": st.adam_step.cpu(), "anchor": st.anchor.cpu(), "best": st.best.cpu(),
+            "agg_counts": torch.tensor(self.agg_counts, dtype=torch.int64),
+            "last_received": torch.tensor([-1 if v is None else v for v in self.last_received], dtype=torch.int64),
+            "vstate": {int(c): [(-1 if s.history_version is None else int(s.history_version)), float(s.history_perf),
+                                int(s.history_round), int(s.rejected_updates)] for c, s in self.vstate.items()},
+            "versions": {int(v): self.versions[v].cpu() for v in vers},
+            "py_rng": _py_state_to_list(self.py_rng.getstate()),
+            "noise_state": self.noise.state.clone() if isinstance(self.noise, TorchRngReplay) else torch.zeros(0),
+            "early": [float(self.early.best), int(self.early.worse)],
+            "last_metrics": torch.from_numpy(self.last_metrics) if self.last_metrics is not None else torch.zeros(0),
+        }
+
+    def save_snapshot(self, path: Optional[str] = None) -> str:
+        base = path or os.path.join(self.cfg.output_root, "Checkpoint", "resume",
+                                    f"{self.cfg.experiment_name}_{self.model_type}_{self.update_type}_run{self.run}.pt")
+        return ckpt.save_resume(self._resume_path(base), self.snapshot())
+
+    def restore(self, s: Dict) -> None:
+        st = self.engine.store
+        self.round_idx = int(s["round_idx"])
+        for k in ("params", "adam_m", "adam_v", "anchor", "best"):
+            getattr(st, k).copy_(s[k].to(st.params.device))
+        st.adam_step.copy_(s["adam_step"].to(st.adam_step.device))
+        self.agg_counts = [int(x) for x in s["agg_counts"].tolist()]
+        self.last_received = [None if v < 0 else int(v) for v in s["last_received"].tolist()]
+        for c, (hv, hp, hr, rej) in s["vstate"].items():
+            self.vstate[int(c)] = VerifierState(None if hv < 0 else hv, hp, hr, rej)
+        self.versions = {int(v): t.to(st.params.device) for v, t in s["versions"].items()}
+        self.py_rng.setstate(_py_state_from_list(s["py_rng"]))
+        if isinstance(self.noise, TorchRngReplay) and s["noise_state"].numel():
+            self.noise.state = s["noise_state"].clone()
+        self.early.best, self.early.worse = float(s["early"][0]), int(s["early"][1])
+        if s["last_metrics"].numel():
+            self.last_metrics = s["last_metrics"].numpy()
+
+
+def _py_state_to_list(state):
+    version, internal, gauss = state
+    return [int(version), list(internal), gauss]
+
+
+def _py_state_from_list(lst):
+    version, internal, gauss = lst
+    return (int(version), tuple(int(x) for x in internal), gauss)

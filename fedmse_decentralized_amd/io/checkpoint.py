@@ -1,0 +1,78 @@
+"""Checkpoint artefacts and resume snapshots.
+
+Reference artefacts (written byte-compatible):
+
+* ``model.cpt`` — legacy (non-zip) torch serialisation of the 8-tensor state
+  dict, written by ``torch.save(..., _use_new_zipfile_serialization=False)``
+  on every validation improvement (`src/Trainer/client_trainer.py:337-350`,
+  SURVEY B.4).  The fused training kernel keeps a device-side best snapshot,
+  so the file is written once per client per round with the same content
+  the reference's last ``save_model`` call produced.
+* ``training_tracking.pkl`` — pickle protocol 4 of ``[(train_loss,
+  valid_loss), ...]`` (`:416`, `:419`, B.4b).
+* ``latent_hybrid_{update}.pkl`` — ``{round: {device: (latent f32 [n, d],
+  labels f32 [n])}}`` consumed by `src/Visualization/latent_visualization.ipynb`
+  (B.5; the writer is absent from the reference snapshot).
+
+New: ``save_resume``/``load_resume`` — a per-round snapshot of every hosted
+client's device state plus the replicated protocol state and RNG states.
+It only holds tensors and plain containers, so it loads with
+``torch.load(weights_only=True)``.
+"""
+from __future__ import annotations
+
+import os
+import pickle
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..models.layout import ModelDims, DEFAULT_DIMS, canonical_to_state_dict, padded_to_canonical
+
+
+def save_model_cpt(save_dir: str, padded_params: torch.Tensor, dims: ModelDims = DEFAULT_DIMS) -> str:
+    os.makedirs(save_dir, exist_ok=True)
+    flat = padded_to_canonical(padded_params.detach().float().cpu(), dims)
+    sd = canonical_to_state_dict(flat, dims)
+    # the reference saves nn.Module.state_dict(): OrderedDict with per-module _metadata
+    from collections import OrderedDict
+
+    state = OrderedDict(sd)
+    meta = OrderedDict()
+    for prefix in ("", "encoder", "encoder.encoder_network", "encoder.encoder_network.0",
+                   "encoder.encoder_network.1", "encoder.encoder_network.2", "decoder",
+                   "decoder.decoder_network", "decoder.decoder_network.0", "decoder.decoder_network.1",
+                   "decoder.decoder_network.2"):
+        meta[prefix] = {"version": 1}
+    state._metadata = meta
+    path = os.path.join(save_dir, "model.cpt")
+    torch.save(state, path, _use_new_zipfile_serialization=False)
+    return path
+
+
+def save_tracking(save_dir: str, tracking: Sequence[Tuple[float, float]]) -> str:
+    os.makedirs(save_dir, exist_ok=True)
+    path = os.path.join(save_dir, "training_tracking.pkl")
+    with open(path, "wb") as f:
+        pickle.dump([(float(a), float(b)) for a, b in tracking], f, protocol=4)
+    return path
+
+
+def save_latents(path: str, data: Dict[int, Dict[str, Tuple[np.ndarray, np.ndarray]]]) -> str:
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "wb") as f:
+        pickle.dump(data, f, protocol=4)
+    return path
+
+
+def save_resume(path: str, payload: Dict) -> str:
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    tmp = path + ".tmp"
+    torch.save(payload, tmp)
+    os.replace(tmp, path)
+    return path
+
+
+def load_resume(path: str) -> Dict:
+    return torch.load(path, map_location="cpu", weights_only=True)

@@ -1,0 +1,632 @@
+// Persistent fused local training of (Shrink-)Autoencoder clients on gfx950.
+//
+// Replaces ClientTrainer.run (src/Trainer/client_trainer.py:360-419): for every
+// selected client, E epochs of mini-batch training (forward, MSE + shrink loss,
+// optional FedProx proximal term, backward, Adam), a validation pass per epoch,
+// patience-based early stopping and the best-model snapshot — all inside ONE
+// launch with no host round trip.  Grid = one 256-thread workgroup (4 wave64,
+// one per SIMD) per client; clients train concurrently on different CUs.
+//
+// Work split inside a workgroup (wave w = 0..3):
+//   * W1a columns d in [32w, 32w+32) and W4a rows d in [32w, 32w+32) are
+//     OWNED by wave w: their Adam state (param, m, v, FedProx anchor) lives in
+//     that wave's VGPRs for the whole launch, in the MFMA accumulator layout of
+//     their gradient tiles, so the optimizer is fused into the gradient
+//     epilogue.  Layer 1 is K-split by the same column block (partial sums
+//     reduced through LDS, barrier #1); layer 4 output / dY rows by the same
+//     row block; dH3 = W4a^T dY is K-split again (barrier #2).
+//   * The 2 KB layers W2a / W3a and their gradients are computed redundantly
+//     (bit-identically) by every wave, each keeping a private copy, so they
+//     need no synchronisation.
+//   * Per training step: 2 workgroup barriers; per validation batch: 1.
+//   * Global memory is touched only to stream the batches (prefetched one step
+//     ahead) and, through LDS staging with coalesced 16-byte accesses, to load
+//     / store the client state and the best-validation snapshot.
+// All products run on v_mfma_f32_16x16x4_f32 (exact fp32).  Batch <= 16 rows
+// (reference default 12, src/main.py:52); padded batch columns and padded
+// features are masked out of the loss and every gradient.
+#include "fedmx_common.h"
+
+namespace fedmx {
+
+struct TrainArgs {
+  float* params;            // [C, P_PAD]
+  float* adam_m;            // [C, P_PAD]
+  float* adam_v;            // [C, P_PAD]
+  const float* anchor;      // [C, P_PAD] FedProx anchor (previous global model)
+  float* best;              // [C, P_PAD] best-validation snapshot (model.cpt content)
+  int32_t* adam_step;       // [C]
+  const float* train_x;     // [rows, DP]
+  const int64_t* train_off; // [C+1]
+  const float* valid_x;     // [rows, DP]
+  const int64_t* valid_off; // [C+1]
+  const int32_t* client_idx;  // [k] store rows to train
+  double* tracking;         // [k, epochs, 2] (train_loss, valid_loss)
+  int32_t* epochs_run;      // [k]
+  int32_t* best_epoch;      // [k]
+  int32_t epochs, batch, patience, d_in, hidden, latent;
+  float lr, beta1, beta2, eps, lambda, mu;
+};
+
+struct AdamStep {
+  float one_m_b1, b2, one_m_b2, bc2s, eps, neg_step_size, two_mu;
+};
+
+template <bool PROX>
+__device__ __forceinline__ void adam_update(float& p, float& m, float& v, float a, float grad, const AdamStep& K,
+                                            float& prox_acc) {
+  float gr = grad;
+  if (PROX) {
+    const float dp = __fsub_rn(p, a);
+    prox_acc = __fmaf_rn(dp, dp, prox_acc);
+    gr = __fadd_rn(gr, __fmul_rn(K.two_mu, dp));
+  }
+  // m.lerp_(g, 1-b1);  v.mul_(b2).addcmul_(g, g, 1-b2)
+  m = __fadd_rn(m, __fmul_rn(K.one_m_b1, __fsub_rn(gr, m)));
+  v = __fadd_rn(__fmul_rn(v, K.b2), __fmul_rn(__fmul_rn(K.one_m_b2, gr), gr));
+  // denom = sqrt(v) / sqrt(bc2) + eps;  p.addcdiv_(m, denom, -step_size)
+  const float den = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), K.bc2s), K.eps);
+  p = __fadd_rn(p, __fmul_rn(K.neg_step_size, __fdiv_rn(m, den)));
+}
+
+// LDS plan (floats); total < 160 KiB -> one workgroup per CU.
+constexpr int L_W1 = HP * S_W1;          // 4224  shared, column block per wave
+constexpr int L_W4 = DP * S_W4;          // 4608  shared, row block per wave
+constexpr int L_W2 = ZP * S_W2;          // 576   per-wave private copy
+constexpr int L_W3 = HP * S_W3;          // 640   per-wave private copy
+constexpr int L_RED = 4 * 2 * 64 * 4;    // 2048  one partial-sum exchange buffer
+constexpr int L_T32 = 32 * S_T;          // 640   [32 features][batch] transpose tile
+constexpr int L_T16 = 16 * S_T;          // 320
+constexpr int L_SCR = 4 * L_T32 + 2 * L_T16;  // 3200 per wave
+constexpr int L_TOTAL = L_W1 + L_W4 + 4 * (L_W2 + L_W3) + 3 * L_RED + 4 * L_SCR + 64;
+
+// Parameter state owned by one lane (MFMA D layouts):
+//   q1[t][v][r] = W1a[16t+4g+r][32w+16v+c]      q4[v][t][r] = W4a[32w+16v+4g+r][16t+c]
+//   q2[t][r]    = W2a[4g+r][16t+c]              q3[t][r]    = W3a[16t+4g+r][c]
+struct Owned {
+  float q1[2][2][4];
+  float q4[2][2][4];
+  float q2[2][4];
+  float q3[2][4];
+};
+
+struct LdsPtrs {
+  float* w1;   // sW1 + 4g*S_W1 + 32w + c       (D-layout element base)
+  float* w4;   // sW4 + (32w+4g)*S_W4 + c
+  float* w2;   // own W2 copy + 4g*S_W2 + c
+  float* w3;   // own W3 copy + 4g*S_W3 + c
+};
+
+__device__ __forceinline__ void owned_to_lds(const Owned& o, const LdsPtrs& L) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        L.w1[(16 * t + r) * S_W1 + 16 * v] = o.q1[t][v][r];
+        L.w4[(16 * v + r) * S_W4 + 16 * t] = o.q4[v][t][r];
+      }
+      L.w2[r * S_W2 + 16 * t] = o.q2[t][r];
+      L.w3[(16 * t + r) * S_W3] = o.q3[t][r];
+    }
+}
+
+__device__ __forceinline__ void lds_to_owned(Owned& o, const LdsPtrs& L) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        o.q1[t][v][r] = L.w1[(16 * t + r) * S_W1 + 16 * v];
+        o.q4[v][t][r] = L.w4[(16 * v + r) * S_W4 + 16 * t];
+      }
+      o.q2[t][r] = L.w2[r * S_W2 + 16 * t];
+      o.q3[t][r] = L.w3[(16 * t + r) * S_W3];
+    }
+}
+
+// dense global [P_PAD] -> LDS masters (W2a/W3a into every wave's copy)
+__device__ __forceinline__ void global_to_masters(const float* __restrict__ src, float* sW1, float* sW4,
+                                                  float* sW23) {
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
+  for (int i = threadIdx.x; i < P_PAD / 4; i += 256) {
+    const f32x4 val = s4[i];
+    int e = i * 4;
+    if (e < OFF_W2) {
+      lds_write4(&sW1[(e / DP) * S_W1 + (e % DP)], val);
+    } else if (e < OFF_W3) {
+      e -= OFF_W2;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) lds_write4(&sW23[ww * (L_W2 + L_W3) + (e / HP) * S_W2 + (e % HP)], val);
+    } else if (e < OFF_W4) {
+      e -= OFF_W3;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww)
+        lds_write4(&sW23[ww * (L_W2 + L_W3) + L_W2 + (e / ZP) * S_W3 + (e % ZP)], val);
+    } else {
+      e -= OFF_W4;
+      lds_write4(&sW4[(e / HP) * S_W4 + (e % HP)], val);
+    }
+  }
+}
+
+// LDS masters -> dense global [P_PAD] (W2a/W3a from wave 0's copy)
+__device__ __forceinline__ void masters_to_global(float* __restrict__ dst, const float* sW1, const float* sW4,
+                                                  const float* sW23) {
+  f32x4* d4 = reinterpret_cast<f32x4*>(dst);
+  for (int i = threadIdx.x; i < P_PAD / 4; i += 256) {
+    int e = i * 4;
+    f32x4 val;
+    if (e < OFF_W2) {
+      val = lds_read4(&sW1[(e / DP) * S_W1 + (e % DP)]);
+    } else if (e < OFF_W3) {
+      e -= OFF_W2;
+      val = lds_read4(&sW23[(e / HP) * S_W2 + (e % HP)]);
+    } else if (e < OFF_W4) {
+      e -= OFF_W3;
+      val = lds_read4(&sW23[L_W2 + (e / ZP) * S_W3 + (e % ZP)]);
+    } else {
+      e -= OFF_W4;
+      val = lds_read4(&sW4[(e / HP) * S_W4 + (e % HP)]);
+    }
+    d4[i] = val;
+  }
+}
+
+template <bool PROX>
+__global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
+  __shared__ __attribute__((aligned(16))) float lds[L_TOTAL];
+  const int w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 15;
+  const int g = lane >> 4;
+  float* const sW1 = lds;
+  float* const sW4 = sW1 + L_W1;
+  float* const sW23 = sW4 + L_W4;                  // 4 x (W2 copy, W3 copy)
+  float* const sW2 = sW23 + w * (L_W2 + L_W3);
+  float* const sW3 = sW2 + L_W2;
+  float* const sRedH1 = sW23 + 4 * (L_W2 + L_W3);  // two buffers (parity)
+  float* const sRedDH3 = sRedH1 + 2 * L_RED;
+  float* const scr = sRedDH3 + L_RED + w * L_SCR;
+  float* const sXT = scr;                // X^T own 32 columns      [32][S_T]
+  float* const sH1T = sXT + L_T32;       // H1^T                    [32][S_T]
+  float* const sT0 = sH1T + L_T32;       // dY^T own rows, then dH3^T
+  float* const sT1 = sT0 + L_T32;        // H3^T, then dH1^T
+  float* const sZT = sT1 + L_T32;        // Z^T (with bias row)     [16][S_T]
+  float* const sDZT = sZT + L_T16;       // dZ^T                    [16][S_T]
+  double* const sLoss = reinterpret_cast<double*>(sRedDH3 + L_RED + 4 * L_SCR);  // [4][4] doubles
+
+  // per-lane bases: D-layout element (write) and A/B-operand (read) addressing
+  LdsPtrs L;
+  L.w1 = sW1 + 4 * g * S_W1 + 32 * w + c;
+  L.w4 = sW4 + (32 * w + 4 * g) * S_W4 + c;
+  L.w2 = sW2 + 4 * g * S_W2 + c;
+  L.w3 = sW3 + 4 * g * S_W3 + c;
+  const float* const a1p = sW1 + c * S_W1 + 32 * w + 4 * g;   // + 16t*S_W1 + 16v
+  const float* const a4p = sW4 + (32 * w + c) * S_W4 + 4 * g;  // + 16v*S_W4 + 16t
+  const float* const a2p = sW2 + c * S_W2 + 4 * g;             // + 16t
+  const float* const a3p = sW3 + c * S_W3 + 4 * g;             // + 16t*S_W3
+  const int tw = 4 * g * S_T + c;   // transpose write: [feature 4g+r (+16v)][b=c]
+  const int tr = c * S_T + 4 * g;   // transpose read : [feature c (+16v)][b=4g..4g+3]
+  float* const redw = sRedDH3 + (w * 2) * 256 + lane * 4;  // own dH3 partial slot (+ t*256)
+
+  const int kslot = blockIdx.x;
+  const int cid = A.client_idx[kslot];
+  float* const Pg = A.params + (size_t)cid * P_PAD;
+  float* const Mg = A.adam_m + (size_t)cid * P_PAD;
+  float* const Vg = A.adam_v + (size_t)cid * P_PAD;
+  float* const Bg = A.best + (size_t)cid * P_PAD;
+  const int d_in = A.d_in, hidden = A.hidden, latent = A.latent;
+
+  // ---- load client state: global -> LDS masters -> owned registers ----------
+  Owned P, M, V, AN;
+  global_to_masters(Mg, sW1, sW4, sW23);
+  __syncthreads();
+  lds_to_owned(M, L);
+  __syncthreads();
+  global_to_masters(Vg, sW1, sW4, sW23);
+  __syncthreads();
+  lds_to_owned(V, L);
+  __syncthreads();
+  if (PROX) {
+    global_to_masters(A.anchor + (size_t)cid * P_PAD, sW1, sW4, sW23);
+    __syncthreads();
+    lds_to_owned(AN, L);
+    __syncthreads();
+  }
+  global_to_masters(Pg, sW1, sW4, sW23);
+  __syncthreads();
+  lds_to_owned(P, L);   // masters keep the live parameters from here on
+
+  const int B = A.batch;
+  const float* const Xtr = A.train_x + (size_t)A.train_off[cid] * DP;
+  const int n_tr = (int)(A.train_off[cid + 1] - A.train_off[cid]);
+  const float* const Xva = A.valid_x + (size_t)A.valid_off[cid] * DP;
+  const int n_va = (int)(A.valid_off[cid + 1] - A.valid_off[cid]);
+  const int nb = (n_tr + B - 1) / B;
+  const int nvb = (n_va + B - 1) / B;
+  int step = A.adam_step[cid];
+  int parity = 0;
+  const bool bias_lane = (w == 3 && g == 3);  // holds X column DP-1 (= 32*3 + 16 + 4*3 + 3)
+  const int xcol = 32 * w + 4 * g;
+
+  auto load_x = [&](const float* X, int row0, int bcur, f32x4& x0, f32x4& x1) {
+    const bool ok = c < bcur;
+    const float* src = X + (size_t)(row0 + c) * DP + xcol;
+    x0 = ok ? *reinterpret_cast<const f32x4*>(src) : zero4();
+    x1 = ok ? *reinterpret_cast<const f32x4*>(src + 16) : zero4();
+    if (bias_lane) x1[3] = 1.f;
+  };
+
+  // Forward of one batch (layer 1 K-split + LDS reduction; layers 2-3 redundant;
+  // layer 4 on own rows).  Adds this lane's loss share (MSE of its own 32
+  // features; shrink term on wave 0 / lane group 0) to `lacc`.
+  auto forward = [&](const f32x4& x0, const f32x4& x1, int bcur, f32x4 (&h1)[2], f32x4& z, f32x4& zb,
+                     f32x4 (&h3)[2], f32x4 (&y)[2], float& norm_c, double& lacc) {
+    float* red = sRedH1 + parity * L_RED;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x4 acc = zero4();
+      const f32x4 a0 = lds_read4(a1p + 16 * t * S_W1);
+      const f32x4 a1 = lds_read4(a1p + 16 * t * S_W1 + 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = mfma16(a0[j], x0[j], acc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = mfma16(a1[j], x1[j], acc);
+      lds_write4(red + (w * 2 + t) * 256 + lane * 4, acc);
+    }
+    __syncthreads();  // barrier #1
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x4 s = lds_read4(red + t * 256 + lane * 4);
+#pragma unroll
+      for (int ww = 1; ww < 4; ++ww) {
+        const f32x4 o = lds_read4(red + (ww * 2 + t) * 256 + lane * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[r] = __fadd_rn(s[r], o[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float vv = fmaxf(s[r], 0.f);
+        if (16 * t + 4 * g + r == HP - 1) vv = 1.f;
+        s[r] = vv;
+      }
+      h1[t] = s;
+    }
+    parity ^= 1;
+    z = zero4();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const f32x4 a = lds_read4(a2p + 16 * t);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) z = mfma16(a[s], h1[t][s], z);
+    }
+    zb = z;
+    if (g == 3) zb[3] = 1.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x4 acc = zero4();
+      const f32x4 a = lds_read4(a3p + 16 * t * S_W3);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = mfma16(a[s], zb[s], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float vv = fmaxf(acc[r], 0.f);
+        if (16 * t + 4 * g + r == HP - 1) vv = 1.f;
+        acc[r] = vv;
+      }
+      h3[t] = acc;
+    }
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f32x4 a = lds_read4(a4p + 16 * v * S_W4 + 16 * t);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma16(a[s], h3[t][s], acc);
+      }
+      y[v] = acc;
+    }
+    float sq = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d0 = y[0][r] - x0[r];
+      const float d1 = y[1][r] - x1[r];
+      sq += (xcol + r < d_in) ? d0 * d0 : 0.f;
+      sq += (xcol + 16 + r < d_in) ? d1 * d1 : 0.f;
+    }
+    sq = (c < bcur) ? sq : 0.f;
+    float nz = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) nz += (4 * g + r < latent) ? z[r] * z[r] : 0.f;
+    nz = sum_lane_groups(nz);
+    norm_c = sqrtf(nz);
+    lacc += (double)sq / ((double)bcur * (double)d_in);
+    if (w == 0 && g == 0 && c < bcur) lacc += (double)A.lambda * (double)norm_c / (double)bcur;
+  };
+
+  AdamStep K;
+  K.one_m_b1 = 1.f - A.beta1;
+  K.b2 = A.beta2;
+  K.one_m_b2 = 1.f - A.beta2;
+  K.eps = A.eps;
+  K.two_mu = 2.f * A.mu;
+  // beta^step as running products (python: 1 - beta ** step)
+  double b1pow = pow((double)A.beta1, (double)step);
+  double b2pow = pow((double)A.beta2, (double)step);
+
+  double min_valid = __builtin_huge_val();
+  int worse = 0, ep_run = 0, best_ep = -1;
+
+  for (int ep = 0; ep < A.epochs; ++ep) {
+    double acc_tr = 0.0;
+    f32x4 xa, xb, na, nbx;
+    if (nb > 0) load_x(Xtr, 0, min(B, n_tr), xa, xb);
+    for (int bi = 0; bi < nb; ++bi) {
+      const int row0 = bi * B;
+      const int bcur = min(B, n_tr - row0);
+      f32x4 h1[2], z, zb, h3[2], y[2];
+      float norm_c;
+      forward(xa, xb, bcur, h1, z, zb, h3, y, norm_c, acc_tr);
+      if (bi + 1 < nb) load_x(Xtr, row0 + B, min(B, n_tr - row0 - B), na, nbx);  // prefetch
+
+      ++step;
+      b1pow *= (double)A.beta1;
+      b2pow *= (double)A.beta2;
+      K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
+      K.bc2s = (float)sqrt(1.0 - b2pow);
+      float prox_acc = 0.f;     // sum (p - anchor)^2 of owned params (pre-update)
+      float prox_acc_sh = 0.f;  // same for the replicated W2a/W3a (counted by wave 0)
+
+      // ---- dY (masked) and the transposes feeding dW4
+      const float scale = 2.0f / (float)(bcur * d_in);
+      f32x4 dy[2];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool okb = c < bcur;
+        dy[0][r] = (okb && xcol + r < d_in) ? (y[0][r] - xa[r]) * scale : 0.f;
+        dy[1][r] = (okb && xcol + 16 + r < d_in) ? (y[1][r] - xb[r]) * scale : 0.f;
+        sT0[tw + r * S_T] = dy[0][r];
+        sT0[tw + (16 + r) * S_T] = dy[1][r];
+        sT1[tw + r * S_T] = h3[0][r];
+        sT1[tw + (16 + r) * S_T] = h3[1][r];
+      }
+      // ---- dH3 partial = W4a(own rows)^T dY(own rows)   (pre-update W4)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 acc = zero4();
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc = mfma16(P.q4[v][t][s], dy[v][s], acc);
+        lds_write4(redw + t * 256, acc);
+      }
+      wave_sync();
+      // ---- dW4 (own rows) + fused Adam
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          f32x4 acc = zero4();
+          const f32x4 a = lds_read4(sT0 + tr + 16 * v * S_T);
+          const f32x4 b = lds_read4(sT1 + tr + 16 * t * S_T);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            adam_update<PROX>(P.q4[v][t][r], M.q4[v][t][r], V.q4[v][t][r], PROX ? AN.q4[v][t][r] : 0.f, acc[r], K,
+                              prox_acc);
+        }
+      // ---- stage X^T, H1^T, Z^T for the remaining weight gradients
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sXT[tw + r * S_T] = xa[r];
+        sXT[tw + (16 + r) * S_T] = xb[r];
+        sH1T[tw + r * S_T] = h1[0][r];
+        sH1T[tw + (16 + r) * S_T] = h1[1][r];
+        sZT[tw + r * S_T] = zb[r];
+      }
+      __syncthreads();  // barrier #2: dH3 partials of all waves visible
+      f32x4 dh3[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 s = lds_read4(sRedDH3 + t * 256 + lane * 4);
+#pragma unroll
+        for (int ww = 1; ww < 4; ++ww) {
+          const f32x4 o = lds_read4(sRedDH3 + (ww * 2 + t) * 256 + lane * 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[r] = __fadd_rn(s[r], o[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = 16 * t + 4 * g + r;
+          s[r] = (h < hidden && h3[t][r] > 0.f) ? s[r] : 0.f;
+          sT0[tw + (16 * t + r) * S_T] = s[r];  // dH3^T (dY^T reads done)
+        }
+        dh3[t] = s;
+      }
+      wave_sync();
+      // ---- dZ = W3a^T dH3 (pre-update W3) ; dW3 = dH3^T Z (redundant) + Adam
+      f32x4 dz = zero4();
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) dz = mfma16(P.q3[t][s], dh3[t][s], dz);
+      {
+        const f32x4 b = lds_read4(sZT + tr);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          f32x4 acc = zero4();
+          const f32x4 a = lds_read4(sT0 + tr + 16 * t * S_T);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            adam_update<PROX>(P.q3[t][r], M.q3[t][r], V.q3[t][r], PROX ? AN.q3[t][r] : 0.f, acc[r], K, prox_acc_sh);
+        }
+      }
+      // shrink-loss gradient: lambda/B * z / ||z|| (0 where ||z|| == 0)
+      const float shr = (c < bcur && norm_c > 0.f) ? A.lambda / ((float)bcur * norm_c) : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dz[r] = (4 * g + r < latent) ? dz[r] + shr * z[r] : 0.f;
+        sDZT[tw + r * S_T] = dz[r];
+      }
+      // ---- dH1 = W2a^T dZ (pre-update W2) -> dH1^T staged in sT1 (H3^T reads done)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 acc = zero4();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma16(P.q2[t][s], dz[s], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = 16 * t + 4 * g + r;
+          sT1[tw + (16 * t + r) * S_T] = (h < hidden && h1[t][r] > 0.f) ? acc[r] : 0.f;
+        }
+      }
+      wave_sync();
+      // ---- dW2 = dZ^T H1 (redundant) + Adam
+      {
+        const f32x4 a = lds_read4(sDZT + tr);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          f32x4 acc = zero4();
+          const f32x4 b = lds_read4(sH1T + tr + 16 * t * S_T);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            adam_update<PROX>(P.q2[t][r], M.q2[t][r], V.q2[t][r], PROX ? AN.q2[t][r] : 0.f, acc[r], K, prox_acc_sh);
+        }
+      }
+      // ---- dW1 (own columns) = dH1^T X + fused Adam
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f32x4 a = lds_read4(sT1 + tr + 16 * t * S_T);
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          f32x4 acc = zero4();
+          const f32x4 b = lds_read4(sXT + tr + 16 * v * S_T);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            adam_update<PROX>(P.q1[t][v][r], M.q1[t][v][r], V.q1[t][v][r], PROX ? AN.q1[t][v][r] : 0.f, acc[r], K,
+                              prox_acc);
+        }
+      }
+      if (PROX) acc_tr += (double)A.mu * (double)(prox_acc + (w == 0 ? prox_acc_sh : 0.f));
+      wave_sync();
+      owned_to_lds(P, L);  // publish the updated parameters (wave-private regions)
+      wave_sync();
+      xa = na;
+      xb = nbx;
+    }
+
+    // ---- validation pass (eval mode, no grad)
+    double acc_va = 0.0;
+    for (int bi = 0; bi < nvb; ++bi) {
+      const int row0 = bi * B;
+      const int bcur = min(B, n_va - row0);
+      f32x4 va, vb;
+      load_x(Xva, row0, bcur, va, vb);
+      f32x4 h1[2], z, zb, h3[2], y[2];
+      float norm_c;
+      forward(va, vb, bcur, h1, z, zb, h3, y, norm_c, acc_va);
+    }
+    double prox_now = 0.0;
+    if (PROX) {
+      float pr = 0.f, prs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int v = 0; v < 2; ++v) {
+            const float d1 = P.q1[t][v][r] - AN.q1[t][v][r];
+            const float d4 = P.q4[v][t][r] - AN.q4[v][t][r];
+            pr += d1 * d1 + d4 * d4;
+          }
+          const float d2 = P.q2[t][r] - AN.q2[t][r];
+          const float d3 = P.q3[t][r] - AN.q3[t][r];
+          prs += d2 * d2 + d3 * d3;
+        }
+      prox_now = (double)pr + (w == 0 ? (double)prs : 0.0);
+    }
+    // ---- epoch-end reduction (fixed order over waves -> identical decision everywhere)
+    {
+      const double s0 = wave_sum_d(acc_tr);
+      const double s1 = wave_sum_d(acc_va);
+      const double s2 = wave_sum_d(prox_now);
+      if (lane == 0) {
+        sLoss[w * 4 + 0] = s0;
+        sLoss[w * 4 + 1] = s1;
+        sLoss[w * 4 + 2] = s2;
+      }
+    }
+    __syncthreads();
+    const double tr_sum = sLoss[0] + sLoss[4] + sLoss[8] + sLoss[12];
+    const double va_sum = sLoss[1] + sLoss[5] + sLoss[9] + sLoss[13];
+    const double px_sum = sLoss[2] + sLoss[6] + sLoss[10] + sLoss[14];
+    const double train_loss = nb > 0 ? tr_sum / nb : __builtin_nan("");
+    double valid_loss = nvb > 0 ? va_sum / nvb : __builtin_nan("");
+    if (PROX) valid_loss += (double)A.mu * px_sum;
+    if (threadIdx.x == 0) {
+      double* trk = A.tracking + ((size_t)kslot * A.epochs + ep) * 2;
+      trk[0] = train_loss;
+      trk[1] = valid_loss;
+    }
+    ep_run = ep + 1;
+    if (valid_loss < min_valid) {
+      min_valid = valid_loss;
+      best_ep = ep;
+      worse = 0;
+      masters_to_global(Bg, sW1, sW4, sW23);  // save_model(): best-validation snapshot
+    } else {
+      ++worse;
+    }
+    __syncthreads();  // sLoss reuse / masters stable for the snapshot copy
+    if (worse >= A.patience && worse > 0) break;
+  }
+
+  // ---- write back: params (masters), then m and v through the same staging
+  masters_to_global(Pg, sW1, sW4, sW23);
+  __syncthreads();
+  owned_to_lds(M, L);
+  __syncthreads();
+  masters_to_global(Mg, sW1, sW4, sW23);
+  __syncthreads();
+  owned_to_lds(V, L);
+  __syncthreads();
+  masters_to_global(Vg, sW1, sW4, sW23);
+  if (threadIdx.x == 0) {
+    A.adam_step[cid] = step;
+    A.epochs_run[kslot] = ep_run;
+    A.best_epoch[kslot] = best_ep;
+  }
+}
+
+}  // namespace fedmx
+
+extern "C" {
+
+int fedmx_train(const void* args, int k, hipStream_t stream) {
+  if (k <= 0) return 0;
+  const fedmx::TrainArgs& A = *reinterpret_cast<const fedmx::TrainArgs*>(args);
+  if (A.batch < 1 || A.batch > 16) return -2;
+  if (A.d_in < 1 || A.d_in > fedmx::DP - 1 || A.hidden < 1 || A.hidden > fedmx::HP - 1 || A.latent < 1 ||
+      A.latent > fedmx::ZP - 1)
+    return -3;
+  if (A.mu != 0.f)
+    hipLaunchKernelGGL(fedmx::train_kernel<true>, dim3(k), dim3(256), 0, stream, A);
+  else
+    hipLaunchKernelGGL(fedmx::train_kernel<false>, dim3(k), dim3(256), 0, stream, A);
+  return (int)hipGetLastError();
+}
+
+int fedmx_train_args_size() { return (int)sizeof(fedmx::TrainArgs); }
+
+}  // extern "C"

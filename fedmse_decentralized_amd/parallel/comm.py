@@ -1,0 +1,173 @@
+"""Communication backends for the decentralised protocol.
+
+The reference has no transport at all: peers are Python objects calling
+each other's methods in one interpreter (`src/Trainer/client_trainer.py:136-151`,
+`src/main.py:259-264`).  Here every rank hosts a shard of the
+clients and the protocol's logical messages become a few collectives per
+round:
+
+* vote scores / dev-set MSEs / epochs-run  -> ``all_reduce_sum`` of a small
+  float64 vector (each entry has exactly one non-zero contributor, so the sum
+  is exact and identical on every rank);
+* model exchange (M2/M4)                   -> ``all_gather`` of the packed,
+  padded parameter vectors of the locally selected clients
+  ([world, slots, 9216] fp32); every rank then runs the same weighted reduce,
+  so no separate broadcast of the aggregate is needed;
+* AUCs / verification results (M6)         -> ``all_reduce_sum``.
+
+Backends:
+* ``LoopbackComm``  – world size 1 (single GPU / CPU runs).
+* ``ThreadComm``    – N in-process ranks on threads (protocol tests without
+  process spawning).
+* ``TorchDistComm`` – ``torch.distributed``; backend ``nccl`` (= RCCL over
+  xGMI on MI355X, one process per GPU) or ``gloo`` (CPU tests).
+"""
+from __future__ import annotations
+
+import threading
+from typing import Any, List, Optional
+
+import torch
+
+
+class Comm:
+    rank: int = 0
+    world_size: int = 1
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+    def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """Returns [world, *t.shape] on t's device."""
+        raise NotImplementedError
+
+    def broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        pass
+
+    def all_gather_object(self, obj: Any) -> List[Any]:
+        raise NotImplementedError
+
+
+class LoopbackComm(Comm):
+    def __init__(self, device: Optional[torch.device] = None):
+        self.rank = 0
+        self.world_size = 1
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+
+    def all_reduce_sum(self, t):
+        return t
+
+    def all_gather(self, t):
+        return t.unsqueeze(0)
+
+    def broadcast(self, t, src):
+        return t
+
+    def all_gather_object(self, obj):
+        return [obj]
+
+
+class _ThreadGroup:
+    def __init__(self, world: int):
+        self.world = world
+        self.barrier = threading.Barrier(world)
+        self.slots: List[Any] = [None] * world
+
+
+class ThreadComm(Comm):
+    """In-process fake collective group; create with ``ThreadComm.group(n)``."""
+
+    def __init__(self, group: _ThreadGroup, rank: int):
+        self.g = group
+        self.rank = rank
+        self.world_size = group.world
+        self.device = torch.device("cpu")
+
+    @staticmethod
+    def group(world: int) -> List["ThreadComm"]:
+        g = _ThreadGroup(world)
+        return [ThreadComm(g, r) for r in range(world)]
+
+    def _exchange(self, obj):
+        self.g.barrier.wait()
+        self.g.slots[self.rank] = obj
+        self.g.barrier.wait()
+        out = list(self.g.slots)
+        self.g.barrier.wait()
+        return out
+
+    def all_reduce_sum(self, t):
+        parts = self._exchange(t.detach().cpu().clone())
+        acc = parts[0].clone()
+        for p in parts[1:]:
+            acc += p
+        return acc.to(t.device)
+
+    def all_gather(self, t):
+        parts = self._exchange(t.detach().cpu().clone())
+        return torch.stack(parts, 0).to(t.device)
+
+    def broadcast(self, t, src):
+        parts = self._exchange(t.detach().cpu().clone())
+        return parts[src].to(t.device)
+
+    def barrier(self):
+        self.g.barrier.wait()
+
+    def all_gather_object(self, obj):
+        return self._exchange(obj)
+
+
+class TorchDistComm(Comm):
+    """torch.distributed collectives on the default process group."""
+
+    def __init__(self, device: Optional[torch.device] = None):
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed is not initialised")
+        self.dist = dist
+        self.rank = dist.get_rank()
+        self.world_size = dist.get_world_size()
+        self.backend = dist.get_backend()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
+        self.device = torch.device(device)
+
+    def _to(self, t):
+        return t if t.device == self.device else t.to(self.device)
+
+    def all_reduce_sum(self, t):
+        x = self._to(t).clone()
+        self.dist.all_reduce(x, op=self.dist.ReduceOp.SUM)
+        return x.to(t.device)
+
+    def all_gather(self, t):
+        x = self._to(t).contiguous()
+        out = torch.empty((self.world_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        self.dist.all_gather_into_tensor(out, x)
+        return out.to(t.device)
+
+    def broadcast(self, t, src):
+        x = self._to(t).clone()
+        self.dist.broadcast(x, src)
+        return x.to(t.device)
+
+    def barrier(self):
+        if self.backend == "nccl":
+            self.dist.barrier(device_ids=[self.device.index])
+        else:
+            self.dist.barrier()
+
+    def all_gather_object(self, obj):
+        out = [None] * self.world_size
+        self.dist.all_gather_object(out, obj)
+        return out

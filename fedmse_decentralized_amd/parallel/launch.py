@@ -1,0 +1,58 @@
+"""Process-group bring-up: one process per GPU (torchrun / torch.distributed.run).
+
+Reads RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT from the
+environment.  On ROCm the ``nccl`` backend is RCCL; for multi-process CPU
+tests use ``gloo``.  ``HSA_ENABLE_IPC_MODE_LEGACY=0`` must stay exported for
+RCCL's dmabuf IPC on this platform.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Optional
+
+import torch
+
+from .comm import Comm, LoopbackComm, TorchDistComm
+
+
+def env_world() -> int:
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def init_comm(backend: Optional[str] = None, device: Optional[str] = None, timeout_s: int = 300) -> Comm:
+    """Create the comm for this process.  World size 1 -> LoopbackComm."""
+    world = env_world()
+    if device is None:
+        device = "cuda" if torch.cuda.is_available() else "cpu"
+    if world <= 1:
+        dev = torch.device("cuda", 0) if device == "cuda" else torch.device("cpu")
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
+        return LoopbackComm(dev)
+    import torch.distributed as dist
+
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if backend is None:
+        backend = "nccl" if device == "cuda" else "gloo"
+    if device == "cuda":
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+    else:
+        dev = torch.device("cpu")
+    if not dist.is_initialized():
+        kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(**kw)
+    return TorchDistComm(dev)
+
+
+def shutdown(comm: Comm) -> None:
+    if isinstance(comm, TorchDistComm):
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.destroy_process_group()

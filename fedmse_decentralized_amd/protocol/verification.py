@@ -1,0 +1,74 @@
+"""Receiver-side verification of a broadcast aggregate.
+
+Reference ``ModelVerifier.verify_model`` (`src/Trainer/model_verifier.py:29-77`)
+and ``ClientTrainer.update_from_peers`` (`src/Trainer/client_trainer.py:174-206`):
+
+* the first model a client ever receives is accepted unconditionally; its
+  performance is recorded as history (Q15);
+* afterwards: ``drift = sum_tensors ||theta_prev_received - theta_new||_2``,
+  ``perf = 1 / (1 + MSE(V, model(V)))``, ``dperf = perf_new - perf_prev``;
+  accept iff ``drift <= 3.0`` and ``dperf >= -0.002``;  the history is
+  updated to the new model either way;
+* accept: adopt the model, refresh the FedProx anchor, reset the rejection
+  counter; reject: increment it, and at ``>= 3`` log a possible attack.
+
+Drift and perf are computed on the device by the engine; the decision and the
+per-client state machine live here (replicated-decision, local-state: each
+rank owns the verifiers of its own clients).
+"""
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass, field
+from typing import Optional
+
+log = logging.getLogger("fedmx")
+
+
+@dataclass
+class VerifierState:
+    history_version: Optional[int] = None   # index of the last received aggregate
+    history_perf: float = 0.0
+    history_round: int = -1
+    rejected_updates: int = 0
+
+
+@dataclass
+class VerifyDecision:
+    verified: bool
+    perf_change: float
+    drift: float
+
+
+class Verifier:
+    def __init__(self, verification_threshold: float = 3.0, performance_threshold: float = 0.002,
+                 method: str = "val", max_rejected: int = 3):
+        self.thr = verification_threshold
+        self.perf_thr = performance_threshold
+        self.method = method
+        self.max_rejected = max_rejected
+
+    def needs_drift(self, st: VerifierState) -> bool:
+        return st.history_version is not None
+
+    def decide(self, client_id: int, st: VerifierState, version: int, perf_new: float, drift: float,
+               current_round: int) -> VerifyDecision:
+        if st.history_version is None:
+            st.history_version, st.history_perf, st.history_round = version, perf_new, current_round
+            return VerifyDecision(True, 0.0, 0.0)
+        change = perf_new - st.history_perf
+        st.history_version, st.history_perf, st.history_round = version, perf_new, current_round
+        log.info(f"Client {client_id} - Param changes: {drift:.10f}, Performance change: {change:.10f}")
+        log.info(f"Using {self.method} dataset for verification")
+        ok = (drift <= self.thr) and (change >= -self.perf_thr)
+        return VerifyDecision(ok, change, drift)
+
+    def apply(self, client_id: int, st: VerifierState, dec: VerifyDecision) -> None:
+        if dec.verified:
+            st.rejected_updates = 0
+            log.info(f"[Client {client_id}] Model verified and updated. Performance change: {dec.perf_change:.10f}")
+        else:
+            st.rejected_updates += 1
+            log.warning(f"[Client {client_id}] Model update rejected. Performance change: {dec.perf_change:.10f}")
+            if st.rejected_updates >= self.max_rejected:
+                log.error(f"[Client {client_id}] Too many rejected updates. Possible attack detected.")

@@ -1,0 +1,83 @@
+"""Replay of the reference's torch-RNG consumption (compat mode).
+
+The reference's only protocol decision that depends on the torch RNG is the
++-0.01 % tie-break noise on vote scores (``torch.rand(1)`` in
+``calculate_mse_score``, `src/Trainer/client_trainer.py:243-245`, SURVEY
+Q17).  Its value depends on every earlier draw from the global CPU
+generator, which the reference consumes as a side effect of (SURVEY
+Appendix C):
+
+* model construction (``nn.Linear`` default init + ``uniform_`` overwrite),
+  once per client at setup and once per ``ModelVerifier._evaluate_model``
+  call (`src/Trainer/model_verifier.py:88-91`, Q16);
+* one ``int64.random_()`` per DataLoader iterator creation (every train and
+  valid epoch loop, every evaluator loop);
+* ``torch.rand(1)`` per vote/MSE score.
+
+Our kernels replace all of that work, so in ``--compat reference`` mode this
+class advances a private copy of the generator by exactly the same draws,
+which makes client selection, elections and hence the whole protocol
+trajectory reproduce the reference for the same seeds.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..models.layout import ModelDims, DEFAULT_DIMS
+
+
+class TorchRngReplay:
+    def __init__(self, state: torch.Tensor, dims: ModelDims = DEFAULT_DIMS):
+        self.state = state.clone()
+        self.dims = dims
+        self.draws = 0
+
+    def _run(self, fn):
+        with torch.random.fork_rng(devices=[]):
+            torch.set_rng_state(self.state)
+            out = fn()
+            self.state = torch.get_rng_state()
+        return out
+
+    def iterators(self, n: int) -> None:
+        if n <= 0:
+            return
+
+        def f():
+            for _ in range(int(n)):
+                torch.empty((), dtype=torch.int64).random_()
+        self._run(f)
+        self.draws += int(n)
+
+    def rand(self) -> float:
+        self.draws += 1
+        return float(self._run(lambda: torch.rand(1).item()))
+
+    def model_inits(self, n: int) -> None:
+        if n <= 0:
+            return
+        from ..models.reference import ReferenceSAE
+
+        def f():
+            for _ in range(int(n)):
+                ReferenceSAE(self.dims, shrink_lambda=0.0)
+        self._run(f)
+        self.draws += int(n)
+
+
+class HostNoise:
+    """Fixed-mode tie-break noise from a seeded numpy generator."""
+
+    def __init__(self, seed: int):
+        import numpy as np
+
+        self.rng = np.random.Generator(np.random.PCG64(seed))
+
+    def iterators(self, n: int) -> None:
+        pass
+
+    def model_inits(self, n: int) -> None:
+        pass
+
+    def rand(self) -> float:
+        return float(self.rng.random())

@@ -1,0 +1,35 @@
+#!/bin/bash
+# One GPU session on the MI355X box: kernel numerics tests, smoke, bench,
+# rocprofv3 kernel statistics.  Every GPU step has its own time limit; the
+# script stops at the first fault / abort / timeout (rc not in {0,1}).
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$ROOT"
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+step() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+MODE=${1:-all}
+python -c "import fedmse_decentralized_amd.ops.build as b; b.build_all()" || exit 3
+if [ "$MODE" = all ] || [ "$MODE" = test ]; then
+  step pytest_gpu 420 python -m pytest tests -m gpu -x -q
+  step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
+  step bench 300 python bench.py --steps 20 --warmup 3 --out "$OUT/bench.json"
+fi
+if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
+  cd /tmp && export TMPDIR=/tmp
+  step rocprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 2
+  cd "$ROOT"
+fi
+echo "=== done"

@@ -1,0 +1,177 @@
+"""Numerics of the hand-written gfx950 kernels vs plain PyTorch fp32/fp64
+references of the same ops (run with ``pytest -m gpu`` on an MI355X)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from fedmse_decentralized_amd.engine.base import TrainHParams
+from fedmse_decentralized_amd.engine.torch_engine import TorchEngine, cen_score_numpy
+from fedmse_decentralized_amd.models.layout import DEFAULT_DIMS, P_PAD, canonical_to_padded, padded_to_canonical
+from fedmse_decentralized_amd.models.reference import init_client_params, rowwise_sse
+from fedmse_decentralized_amd.ops import _hip, _host
+
+DEV = torch.device("cuda", 0)
+
+
+def _engine():
+    from fedmse_decentralized_amd.engine.hip_engine import HipEngine
+
+    return HipEngine(DEFAULT_DIMS, DEV)
+
+
+def _data(n, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.zeros(n, 128)
+    x[:, :115] = torch.randn(n, 115, generator=g) * scale
+    return x
+
+
+def test_native_library_is_loaded():
+    import ctypes
+
+    L = _hip.lib()
+    assert isinstance(L, ctypes.CDLL)
+    assert "libfedmx_hip.so" in L._name
+
+
+def test_mfma_f32_16x16x4_lane_layout():
+    D = _hip.probe_mfma(DEV)
+    i = np.arange(16)
+    A = i[:, None] + 100.0 * np.arange(4)[None, :]
+    B = 1000.0 * np.arange(4)[:, None] + i[None, :]
+    assert np.array_equal(D, A @ B)
+
+
+def test_forward_rows_matches_torch():
+    params, _ = init_client_params(3, 7)
+    params = params + 0.05 * torch.randn(params.shape, generator=torch.Generator().manual_seed(1))
+    pad = canonical_to_padded(params).to(DEV)
+    xs = [_data(n, seed=n).to(DEV) for n in (1, 17, 300, 12)]
+    items = [(0, xs[0]), (1, xs[1]), (2, xs[2]), (1, xs[3])]
+    sse, lat = _hip.forward_rows(pad, items, DEFAULT_DIMS, True, True)
+    for (row, x), s, z in zip(items, sse, lat):
+        rs, rz = rowwise_sse(params[row].double(), x[:, :115].cpu().double())
+        torch.testing.assert_close(s.cpu().double(), rs, rtol=2e-5, atol=1e-5)
+        torch.testing.assert_close(z.cpu().double(), rz, rtol=2e-5, atol=1e-5)
+
+
+def test_weighted_sum_and_drift():
+    g = torch.Generator().manual_seed(2)
+    stack = canonical_to_padded(torch.randn(5, DEFAULT_DIMS.num_params, generator=g)).to(DEV)
+    w = [0.1, 0.3, 0.2, 0.25, 0.15]
+    out = _hip.weighted_sum(stack, w)
+    ref = torch.zeros(P_PAD)
+    for k in range(5):
+        ref = ref + stack[k].cpu() * torch.tensor(w[k], dtype=torch.float32)
+    assert torch.equal(out.cpu(), ref)
+    eng = _engine()
+    d = eng.param_drift(stack[:3], stack[4])
+    tref = TorchEngine(DEFAULT_DIMS, torch.device("cpu")).param_drift(stack[:3].cpu(), stack[4].cpu())
+    torch.testing.assert_close(d.cpu(), tref, rtol=1e-5, atol=1e-5)
+
+
+def test_standardize_ddof1():
+    x = (_data(170, seed=3, scale=4.0) + 2.0)
+    x[:, 115:] = 0
+    y = _hip.standardize_ddof1(x.to(DEV), 115).cpu()
+    xr = x[:, :115].double()
+    ref = (xr - xr.mean(0)) / (xr.std(0) + 1e-8)
+    torch.testing.assert_close(y[:, :115].double(), ref, rtol=1e-5, atol=1e-5)
+    assert torch.count_nonzero(y[:, 115:]) == 0
+
+
+def test_cen_scores_and_auc():
+    rng = np.random.default_rng(4)
+    tr = (rng.normal(size=(680, 7)) * 3 + 1).astype(np.float32)
+    te = (rng.normal(size=(3900, 7)) * 5).astype(np.float32)
+    eng = _engine()
+    out = eng.cen_scores([torch.from_numpy(tr).to(DEV)], [torch.from_numpy(te).to(DEV)])[0].cpu().numpy()
+    ref = cen_score_numpy(tr, te)
+    np.testing.assert_allclose(out, ref, rtol=1e-12, atol=1e-12)
+    y = rng.integers(0, 2, size=3900).astype(np.int32)
+    s = np.round(out + y * 0.5, 1)  # ties
+    got = eng.auc([torch.from_numpy(s).to(DEV)], [torch.from_numpy(y).to(DEV)])
+    assert abs(got[0] - _host.roc_auc(s, y)) < 1e-12
+    s32 = torch.from_numpy(s.astype(np.float32)).to(DEV)
+    got32 = eng.auc([s32], [torch.from_numpy(y).to(DEV)])
+    assert abs(got32[0] - _host.roc_auc(s.astype(np.float32).astype(np.float64), y)) < 1e-12
+
+
+def _setup_pair(n_train=(53, 40), n_valid=(14, 9), seed=0):
+    from fedmse_decentralized_amd.engine.hip_engine import HipEngine
+
+    rng = np.random.default_rng(seed)
+    tr = [rng.normal(size=(n, 115)).astype(np.float32) for n in n_train]
+    va = [rng.normal(size=(n, 115)).astype(np.float32) for n in n_valid]
+    te = [rng.normal(size=(20, 115)).astype(np.float32) for _ in n_train]
+    lab = [np.r_[np.zeros(10), np.ones(10)].astype(np.int64) for _ in n_train]
+    init, _ = init_client_params(len(n_train), seed)
+    ref = TorchEngine(DEFAULT_DIMS, torch.device("cpu"))
+    ref.setup(tr, va, te, lab, init)
+    hip = HipEngine(DEFAULT_DIMS, DEV)
+    hip.setup(tr, va, te, lab, init)
+    return ref, hip
+
+
+@pytest.mark.parametrize("lam,mu,batch", [(5.0, 0.0, 12), (0.0, 0.0, 12), (5.0, 0.001, 12), (10.0, 0.0, 16),
+                                          (1.0, 0.01, 7)])
+def test_train_kernel_matches_torch_engine(lam, mu, batch):
+    ref, hip = _setup_pair()
+    # non-trivial FedProx anchor
+    anchor = ref.store.params + 0.01 * torch.randn(ref.store.params.shape, generator=torch.Generator().manual_seed(5))
+    anchor = canonical_to_padded(padded_to_canonical(anchor))
+    ref.store.anchor.copy_(anchor)
+    hip.store.anchor.copy_(anchor.to(DEV))
+    hp = TrainHParams(epochs=3, batch_size=batch, lr=1e-3, shrink_lambda=lam, fedprox_mu=mu, patience=1)
+    r1 = ref.train([0, 1], hp)
+    r2 = hip.train([0, 1], hp)
+    assert list(r1.epochs_run) == list(r2.epochs_run)
+    assert list(r1.best_epoch) == list(r2.best_epoch)
+    for a, b in zip(r1.tracking, r2.tracking):
+        np.testing.assert_allclose(np.array(b), np.array(a), rtol=2e-4, atol=1e-6)
+    torch.testing.assert_close(hip.store.params.cpu(), ref.store.params, rtol=2e-3, atol=2e-5)
+    torch.testing.assert_close(hip.store.best.cpu(), ref.store.best, rtol=2e-3, atol=2e-5)
+    torch.testing.assert_close(hip.store.adam_m.cpu(), ref.store.adam_m, rtol=5e-3, atol=1e-6)
+    torch.testing.assert_close(hip.store.adam_v.cpu(), ref.store.adam_v, rtol=5e-3, atol=1e-9)
+    assert torch.equal(hip.store.adam_step.cpu(), ref.store.adam_step)
+    # padding stays exactly zero
+    from fedmse_decentralized_amd.models.layout import real_mask_padded
+
+    pad = ~real_mask_padded().to(DEV)
+    assert torch.count_nonzero(hip.store.params[:, pad]) == 0
+
+
+def test_train_kernel_single_step_tight():
+    # one Adam step from identical state: errors are pure fp32 rounding
+    ref, hip = _setup_pair(n_train=(12,), n_valid=(12,), seed=3)
+    hp = TrainHParams(epochs=1, batch_size=12, lr=1e-3, shrink_lambda=5.0, patience=1)
+    ref.train([0], hp)
+    hip.train([0], hp)
+    torch.testing.assert_close(hip.store.params.cpu(), ref.store.params, rtol=1e-4, atol=1e-6)
+
+
+def test_train_kernel_many_clients_concurrently():
+    from fedmse_decentralized_amd.engine.hip_engine import HipEngine
+
+    rng = np.random.default_rng(9)
+    C = 40
+    tr = [rng.normal(size=(int(rng.integers(20, 80)), 115)).astype(np.float32) for _ in range(C)]
+    va = [rng.normal(size=(int(rng.integers(5, 20)), 115)).astype(np.float32) for _ in range(C)]
+    te = [rng.normal(size=(10, 115)).astype(np.float32) for _ in range(C)]
+    lab = [np.r_[np.zeros(5), np.ones(5)].astype(np.int64) for _ in range(C)]
+    init, _ = init_client_params(C, 1)
+    hip = HipEngine(DEFAULT_DIMS, DEV)
+    hip.setup(tr, va, te, lab, init)
+    hp = TrainHParams(epochs=2, batch_size=12, lr=1e-3, shrink_lambda=5.0, patience=1)
+    sel = list(range(0, C, 3))
+    res = hip.train(sel, hp)
+    # each client's result equals training it alone
+    solo = HipEngine(DEFAULT_DIMS, DEV)
+    solo.setup(tr, va, te, lab, init)
+    for c in sel[:4]:
+        solo.train([c], hp)
+        assert torch.equal(solo.store.params[c], hip.store.params[c])
+    untouched = [c for c in range(C) if c not in sel]
+    assert torch.equal(hip.store.params[untouched].cpu(), canonical_to_padded(init[untouched]))

@@ -1,0 +1,76 @@
+"""Packed layouts and the torch reference model."""
+import numpy as np
+import pytest
+import torch
+
+from fedmse_decentralized_amd.models.layout import (
+    DEFAULT_DIMS, P_PAD, ModelDims, canonical_to_padded, padded_index, padded_to_canonical, padded_views,
+    real_mask_padded, segment_ids_padded, state_dict_to_canonical, canonical_to_state_dict, STATE_KEYS)
+from fedmse_decentralized_amd.models.reference import ReferenceSAE, init_client_params, functional_forward, unflatten
+
+
+def test_param_count_matches_reference():
+    # 115->27->7->27->115 = 6,764 fp32
+    assert DEFAULT_DIMS.num_params == 6764
+    assert P_PAD == 9216
+
+
+def test_roundtrip_and_segments():
+    g = torch.Generator().manual_seed(0)
+    flat = torch.randn(3, DEFAULT_DIMS.num_params, generator=g)
+    pad = canonical_to_padded(flat)
+    assert pad.shape == (3, P_PAD)
+    assert torch.equal(padded_to_canonical(pad), flat)
+    mask = real_mask_padded()
+    assert int(mask.sum()) == 6764
+    assert torch.count_nonzero(pad[:, ~mask]) == 0
+    seg = segment_ids_padded(DEFAULT_DIMS)
+    counts = [int((seg == t).sum()) for t in range(8)]
+    assert counts == [27 * 115, 27, 7 * 27, 7, 27 * 7, 27, 115 * 27, 115]
+
+
+def test_augmented_matrices_compute_the_same_forward():
+    m = ReferenceSAE(DEFAULT_DIMS, shrink_lambda=5.0)
+    flat = state_dict_to_canonical(m.state_dict())
+    W1, W2, W3, W4 = padded_views(canonical_to_padded(flat))
+    x = torch.randn(12, 115, dtype=torch.float64)
+    xa = torch.zeros(12, 128, dtype=torch.float64)
+    xa[:, :115] = x
+    xa[:, 127] = 1
+    h1 = torch.relu(xa @ W1.double().T)
+    h1[:, 31] = 1
+    z = h1 @ W2.double().T
+    zb = z.clone()
+    zb[:, 15] = 1
+    h3 = torch.relu(zb @ W3.double().T)
+    h3[:, 31] = 1
+    y = h3 @ W4.double().T
+    with torch.no_grad():
+        zr, yr = functional_forward([t.double() for t in unflatten(flat)], x)
+    assert torch.allclose(z[:, :7], zr, atol=1e-12)
+    assert torch.allclose(y[:, :115], yr, atol=1e-12)
+
+
+def test_state_dict_keys_and_init_distribution():
+    m = ReferenceSAE(DEFAULT_DIMS)
+    assert list(m.state_dict().keys()) == list(STATE_KEYS)
+    params, state = init_client_params(4, 0)
+    assert params.shape == (4, 6764)
+    sd = canonical_to_state_dict(params[0])
+    # reference init: U(+-1/sqrt(fan_in)) weights, zero bias
+    assert float(sd[STATE_KEYS[0]].abs().max()) <= 1 / np.sqrt(115) + 1e-7
+    assert float(sd[STATE_KEYS[4]].abs().max()) <= 1 / np.sqrt(7) + 1e-7
+    for k in STATE_KEYS[1::2]:
+        assert torch.count_nonzero(sd[k]) == 0
+    # deterministic, and identical to building the modules in order
+    p2, _ = init_client_params(4, 0)
+    assert torch.equal(params, p2)
+    torch.manual_seed(0)
+    ref = [state_dict_to_canonical(ReferenceSAE(DEFAULT_DIMS).state_dict()) for _ in range(4)]
+    assert torch.equal(params, torch.stack(ref))
+
+
+def test_dims_limits():
+    with pytest.raises(ValueError):
+        ModelDims(128, 27, 7)
+    ModelDims(46, 27, 7)  # CIC-style feature count is supported
