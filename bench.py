@@ -97,6 +97,7 @@ def main(argv=None):
     last = None
     for _ in range(args.steps):
         last = one_round()
+    fed.writer.flush()   # artefacts of the timed rounds are on disk before the clock stops
     comm.barrier()
     if device == "cuda":
         torch.cuda.synchronize()

@@ -2,26 +2,32 @@
 
 An *engine* owns the clients hosted by one rank (one GPU): their datasets,
 parameters and optimiser state, all resident on the device in
-structure-of-arrays form, and exposes the compute primitives the federated
-protocol needs:
+structure-of-arrays form, and exposes the compute the federated protocol
+needs.  Two levels:
 
-* ``train``          – local training of a set of clients (reference
-  ``ClientTrainer.run``, `src/Trainer/client_trainer.py:360-419`);
-* ``forward_rows``   – per-row squared reconstruction error and/or latents of
-  (parameter-vector, dataset) pairs: vote scores, FedMSE weights,
-  verification, AE anomaly scores, SAE latents
-  (`src/Trainer/client_trainer.py:208-247`, `:115-130`,
-  `src/Trainer/model_verifier.py:86-99`, `src/Evaluator/evaluator.py:52-94`);
-* ``weighted_sum``   – FedAvg / MSEAvg reduction (`client_trainer.py:107-134`);
-* ``param_drift``    – verifier drift, sum of per-tensor L2 norms
-  (`src/Trainer/model_verifier.py:79-84`);
-* ``cen_scores`` + ``auc`` – SAE-CEN scoring and ROC-AUC
-  (`src/Model/Centroid.py:15-35`, `src/Evaluator/evaluator.py:21-28`).
+Primitives
+  * ``train_launch`` / ``train_collect`` – local training of a set of clients
+    (reference ``ClientTrainer.run``, `src/Trainer/client_trainer.py:360-419`);
+  * ``forward_rows``   – per-row squared reconstruction error and/or latents of
+    (parameter-vector, dataset) pairs (`client_trainer.py:208-247`, `:115-130`,
+    `src/Trainer/model_verifier.py:86-99`, `src/Evaluator/evaluator.py:52-94`);
+  * ``weighted_sum``   – FedAvg / MSEAvg reduction (`client_trainer.py:107-134`);
+  * ``param_drift``    – verifier drift (`model_verifier.py:79-84`);
+  * ``cen_scores`` + ``auc`` – SAE-CEN scoring and ROC-AUC
+    (`src/Model/Centroid.py:15-35`, `src/Evaluator/evaluator.py:21-28`).
 
-Two implementations: ``TorchEngine`` (pure PyTorch, reference-exact math,
-runs anywhere) and ``HipEngine`` (hand-written gfx950 kernels).  The HIP
-engine never falls back to torch for these primitives: if its library is
-missing it raises.
+Round operations (what the federation calls; results stay on the device
+until one ``fetch`` per protocol phase):
+  * ``vote_scores`` – vote score on the standardised vote data + dev-set MSE
+    for each given client;
+  * ``verify_stats`` – MSE of the aggregate on the verification sets + drift
+    against the previously received aggregates;
+  * ``adopt`` – copy the aggregate into accepted clients (+ FedProx anchor);
+  * ``evaluate`` – detection metric of every hosted client.
+
+``TorchEngine`` implements the primitives with reference-exact PyTorch math;
+``HipEngine`` runs everything on hand-written gfx950 kernels and never falls
+back to torch for them.
 """
 from __future__ import annotations
 
@@ -55,6 +61,13 @@ class TrainResult:
     best_epoch: np.ndarray               # int [k] (-1 if never improved)
 
 
+@dataclass
+class TrainHandle:
+    local_ids: List[int]
+    tensors: List[torch.Tensor] = field(default_factory=list)   # device results to fetch
+    result: Optional[TrainResult] = None                        # filled synchronously by eager engines
+
+
 def pad_features(x: np.ndarray) -> np.ndarray:
     """[n, D] -> [n, DP] float32, zero padded (aligned 512-byte rows)."""
     n, d = x.shape
@@ -82,7 +95,6 @@ class ClientStore:
         self.adam_step = torch.zeros(C, dtype=torch.int32, device=device)
         self.anchor = torch.zeros(C, P_PAD, **f32)
         self.best = torch.zeros(C, P_PAD, **f32)
-        # data: concatenated, row-padded to DP columns
         self.train = self.valid = self.test = None
         self.train_off = self.valid_off = self.test_off = None
         self.test_label = None
@@ -112,6 +124,24 @@ class ClientStore:
     def labels(self, c: int) -> np.ndarray:
         return self.test_label_np[int(self.test_off[c]):int(self.test_off[c + 1])]
 
+    def label_view(self, c: int) -> torch.Tensor:
+        return self.test_label[int(self.test_off[c]):int(self.test_off[c + 1])]
+
+
+def batch_mean_scores(sse: torch.Tensor, bs: int, d_in: int) -> Tuple[float, float]:
+    """(mean over batches of the batch MSE, overall MSE) of a per-row SSE vector
+    (`src/Trainer/client_trainer.py:226-241`)."""
+    x = sse.detach().double().cpu().numpy()
+    n = x.shape[0]
+    if n == 0:
+        return float("inf"), float("nan")
+    tot, nb = 0.0, 0
+    for s in range(0, n, bs):
+        seg = x[s:s + bs]
+        tot += float(seg.sum() / (seg.shape[0] * d_in))
+        nb += 1
+    return tot / nb, float(x.sum() / (n * d_in))
+
 
 class Engine:
     name = "abstract"
@@ -137,8 +167,18 @@ class Engine:
     def canonical(self, padded: torch.Tensor) -> torch.Tensor:
         return padded_to_canonical(padded, self.dims)
 
+    def fetch(self, tensors: Sequence[torch.Tensor]) -> List[np.ndarray]:
+        """Device -> host for several results with (at most) one synchronisation."""
+        return [t.detach().cpu().numpy() for t in tensors]
+
     # -- primitives (implemented by subclasses) --------------------------------
     def train(self, local_ids: Sequence[int], hp: TrainHParams) -> TrainResult:
+        return self.train_collect(self.train_launch(local_ids, hp))
+
+    def train_launch(self, local_ids: Sequence[int], hp: TrainHParams) -> TrainHandle:
+        raise NotImplementedError
+
+    def train_collect(self, handle: TrainHandle, host: Optional[List[np.ndarray]] = None) -> TrainResult:
         raise NotImplementedError
 
     def forward_rows(self, params: torch.Tensor, items: Sequence[Tuple[int, torch.Tensor]],
@@ -163,6 +203,50 @@ class Engine:
         """(x - mean) / (std_ddof1 + 1e-8) over the real D columns
         (`src/Trainer/client_trainer.py:220-223`)."""
         raise NotImplementedError
+
+    # -- round operations (defaults in terms of the primitives) -----------------
+    def vote_scores(self, local_rows: Sequence[int], vote_data: torch.Tensor, dev_set: Optional[torch.Tensor],
+                    vote_bs: int) -> torch.Tensor:
+        """float64 [k, 2]: (vote score on standardised vote data, dev-set MSE or nan)."""
+        k = len(local_rows)
+        out = torch.full((k, 2), float("nan"), dtype=torch.float64)
+        if k == 0:
+            return out
+        vs = self.standardize_ddof1(vote_data)
+        items = [(c, vs) for c in local_rows]
+        if dev_set is not None:
+            items += [(c, dev_set) for c in local_rows]
+        sse, _ = self.forward_rows(self.store.params, items, want_sse=True)
+        D = self.dims.d_in
+        for i in range(k):
+            out[i, 0] = batch_mean_scores(sse[i], vote_bs, D)[0]
+            if dev_set is not None:
+                out[i, 1] = batch_mean_scores(sse[k + i], 1 << 30, D)[1]
+        return out
+
+    def verify_stats(self, agg: torch.Tensor, datasets: Sequence[torch.Tensor], hist: Optional[torch.Tensor]):
+        """(MSE of ``agg`` on each dataset [float64], drift of each hist row vs agg)."""
+        aggp = agg.unsqueeze(0)
+        sse, _ = self.forward_rows(aggp, [(0, x) for x in datasets], want_sse=True) if datasets else ([], None)
+        D = self.dims.d_in
+        mse = torch.tensor([batch_mean_scores(s, 1 << 30, D)[1] for s in sse], dtype=torch.float64)
+        drift = self.param_drift(hist, agg) if hist is not None and hist.shape[0] else torch.zeros(0)
+        return mse, drift
+
+    def adopt(self, local_rows: Sequence[int], agg: torch.Tensor, anchor: bool = True) -> None:
+        st = self.store
+        if not len(local_rows):
+            return
+        idx = torch.tensor(list(local_rows), dtype=torch.long, device=st.params.device)
+        rows = agg.unsqueeze(0).expand(len(local_rows), -1)
+        st.params.index_copy_(0, idx, rows)
+        if anchor:
+            st.anchor.index_copy_(0, idx, rows)
+
+    def evaluate(self, model_type: str, metric: str = "AUC", keep_latents: bool = False):
+        from ..eval.evaluator import evaluate_clients
+
+        return evaluate_clients(self, list(range(self.store.num_clients)), model_type, metric, keep_latents)
 
     def synchronize(self):
         if self.device.type == "cuda":

@@ -1,25 +1,32 @@
 """HIP engine: every compute primitive on hand-written gfx950 kernels.
 
-* ``train``        -> ``fedmx_train`` (persistent fused local training, one
-                      workgroup per client, all selected clients in one launch)
-* ``forward_rows`` -> ``fedmx_forward_rows`` (any list of model x row-block
-                      pairs in one launch)
-* ``weighted_sum`` -> ``fedmx_weighted_sum``;  ``param_drift`` -> ``fedmx_param_drift``
-* ``cen_scores``   -> ``fedmx_cen_score``;     ``auc`` -> ``fedmx_auc``
-* ``standardize_ddof1`` -> ``fedmx_standardize_ddof1``
+* ``train_launch``  -> ``fedmx_train`` (persistent fused local training, one
+                       workgroup per client, all selected clients in one launch;
+                       results stay on the device until the next ``fetch``)
+* ``forward_rows``  -> ``fedmx_forward_rows`` (any list of model x row-block pairs)
+* ``vote_scores``   -> ``fedmx_standardize_lds`` + ``fedmx_forward_rows`` +
+                       ``fedmx_score_reduce`` (3 launches, no host sync)
+* ``verify_stats``  -> ``fedmx_forward_rows`` + ``fedmx_score_reduce`` + ``fedmx_param_drift``
+* ``adopt``         -> ``fedmx_broadcast_rows``
+* ``evaluate``      -> cached plans: ``fedmx_forward_rows`` (latents / SSE of every
+                       hosted client) + ``fedmx_cen_score`` + ``fedmx_auc``
+* ``weighted_sum``  -> ``fedmx_weighted_sum``
 
-The kernels have no PyTorch fallback: a missing or failing library raises.
+Descriptor arrays are cached on the device for static work and streamed
+through a pinned ring otherwise; device->host traffic goes through a pinned
+stage with one event wait per protocol phase.  There is no PyTorch fallback:
+a missing or failing library raises.
 """
 from __future__ import annotations
 
-from typing import Sequence
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
 
-from ..models.layout import segment_ids_padded
+from ..models.layout import P_PAD, segment_ids_padded
 from ..ops import _hip, _host
-from .base import Engine, TrainHParams, TrainResult
+from .base import Engine, TrainHandle, TrainHParams, TrainResult
 
 
 class HipEngine(Engine):
@@ -31,19 +38,50 @@ class HipEngine(Engine):
             raise RuntimeError("HipEngine requires a GPU device")
         _hip.lib()  # load (and fail loudly) up front
         self._seg = segment_ids_padded(dims).to(self.device)
+        self._stage = _hip.HostStage(self.device)
+        self._eval_plans: Dict[str, dict] = {}
+        self._vs = None
 
-    def train(self, local_ids: Sequence[int], hp: TrainHParams) -> TrainResult:
-        tracking, epochs_run, best_epoch, _ = _hip.train(self.store, list(local_ids), hp, self.dims)
-        tr = tracking.cpu().numpy()
-        er = epochs_run.cpu().numpy().astype(np.int64)
-        be = best_epoch.cpu().numpy().astype(np.int64)
-        track = [[(float(tr[i, e, 0]), float(tr[i, e, 1])) for e in range(int(er[i]))] for i in range(len(local_ids))]
-        return TrainResult(list(local_ids), er, track, be)
+    def setup(self, *a, **k):
+        super().setup(*a, **k)
+        self._eval_plans = {}
+        self.store._train_bufs = None
+
+    # -- transfers -----------------------------------------------------------------
+    def fetch(self, tensors: Sequence[torch.Tensor]) -> List[np.ndarray]:
+        out: List[Optional[np.ndarray]] = [None] * len(tensors)
+        dev_idx = []
+        for i, t in enumerate(tensors):
+            if t.device.type == "cpu":
+                out[i] = t.detach().numpy()
+            else:
+                dev_idx.append(i)
+                self._stage.add(t)
+        if dev_idx:
+            res = self._stage.fetch()
+            for i, r in zip(dev_idx, res):
+                out[i] = r
+        return out
+
+    # -- training ------------------------------------------------------------------
+    def train_launch(self, local_ids: Sequence[int], hp: TrainHParams) -> TrainHandle:
+        trk, er, be = _hip.train(self.store, list(local_ids), hp, self.dims, getattr(self.store, "_train_bufs", None))
+        return TrainHandle(list(local_ids), [trk, er, be])
+
+    def train_collect(self, handle: TrainHandle, host: Optional[List[np.ndarray]] = None) -> TrainResult:
+        if host is None:
+            host = self.fetch(handle.tensors)
+        tr, er, be = host
+        er = er.astype(np.int64)
+        track = [[(float(tr[i, e, 0]), float(tr[i, e, 1])) for e in range(int(er[i]))]
+                 for i in range(len(handle.local_ids))]
+        return TrainResult(handle.local_ids, er, track, be.astype(np.int64))
 
     def train_async(self, local_ids: Sequence[int], hp: TrainHParams):
-        """Launch without reading results back (bench / overlap)."""
-        return _hip.train(self.store, list(local_ids), hp, self.dims)
+        """Launch without reading results back (benchmarks)."""
+        return self.train_launch(local_ids, hp)
 
+    # -- primitives ----------------------------------------------------------------
     def forward_rows(self, params, items, want_sse=True, want_latent=False):
         if not items:
             return [], []
@@ -59,8 +97,10 @@ class HipEngine(Engine):
         return _hip.cen_scores(train_lat, test_lat, self.dims.latent)
 
     def auc(self, scores, labels):
-        f32_scale = 1.0
-        out = _hip.auc(list(scores), list(labels), f32_scale).cpu().numpy()
+        out = self.fetch([_hip.auc(list(scores), list(labels))])[0]
+        return self._auc_fixup(out, scores, labels)
+
+    def _auc_fixup(self, out, scores, labels):
         for i in np.flatnonzero(out == -1.0):   # class too large for the LDS sort: exact host path
             s = scores[i].detach().double().cpu().numpy()
             out[i] = _host.roc_auc(np.nan_to_num(s), labels[i].cpu().numpy())
@@ -68,3 +108,96 @@ class HipEngine(Engine):
 
     def standardize_ddof1(self, x):
         return _hip.standardize_ddof1(x.contiguous(), self.dims.d_in)
+
+    # -- round operations ------------------------------------------------------------
+    def vote_scores(self, local_rows, vote_data, dev_set, vote_bs):
+        k = len(local_rows)
+        if k == 0:
+            return torch.zeros(0, 2, dtype=torch.float64, device=self.device)
+        if self._vs is None or self._vs.shape[0] < vote_data.shape[0]:
+            self._vs = torch.empty(max(vote_data.shape[0], 256), 128, dtype=torch.float32, device=self.device)
+        vs = self._vs[:vote_data.shape[0]]
+        _hip.standardize_ddof1(vote_data.contiguous(), self.dims.d_in, out=vs)
+        items = [(c, vs) for c in local_rows]
+        if dev_set is not None:
+            items += [(c, dev_set) for c in local_rows]
+        sse, _ = _hip.forward_rows(self.store.params, items, self.dims, True, False)
+        red = _hip.score_reduce(sse, [vote_bs] * k + [0] * (len(sse) - k), self.dims.d_in)
+        out = torch.full((k, 2), float("nan"), dtype=torch.float64, device=self.device)
+        out[:, 0] = red[:k, 0]
+        if dev_set is not None:
+            out[:, 1] = red[k:, 1]
+        return out
+
+    def verify_stats(self, agg, datasets, hist):
+        if datasets:
+            sse, _ = _hip.forward_rows(agg.unsqueeze(0), [(0, x) for x in datasets], self.dims, True, False)
+            mse = _hip.score_reduce(sse, [0] * len(sse), self.dims.d_in)[:, 1]
+        else:
+            mse = torch.zeros(0, dtype=torch.float64, device=self.device)
+        drift = self.param_drift(hist, agg) if hist is not None and hist.shape[0] else \
+            torch.zeros(0, dtype=torch.float32, device=self.device)
+        return mse, drift
+
+    def adopt(self, local_rows, agg, anchor=True):
+        st = self.store
+        _hip.broadcast_rows(st.params, st.anchor if anchor else None, list(local_rows), agg)
+
+    def _plan(self, model_type: str) -> dict:
+        p = self._eval_plans.get(model_type)
+        if p is not None:
+            return p
+        st = self.store
+        C = st.num_clients
+        labels = [st.label_view(c) for c in range(C)]
+        aucs = torch.empty(C, dtype=torch.float64, device=self.device)
+        if model_type == "hybrid":
+            items = []
+            for c in range(C):
+                items += [(c, st.rows("train", c)), (c, st.rows("test", c))]
+            fwd = _hip.FwdPlan(st.params, items, self.dims, want_sse=False, want_latent=True)
+            lat = fwd.lat_views()
+            scores_all = torch.empty(sum(int(st.test_off[c + 1] - st.test_off[c]) for c in range(C)),
+                                     dtype=torch.float64, device=self.device)
+            cdesc, scores = _hip.cen_desc(lat[0::2], lat[1::2], scores_all, self.dims.latent)
+            cdesc_dev = torch.from_numpy(cdesc.view(np.uint8).copy()).to(self.device)
+            adesc = _hip.auc_desc(scores, labels, aucs, 1.0)
+            p = dict(fwd=fwd, cen=cdesc_dev, ncen=C, scores=scores, test_lat=lat[1::2])
+        elif model_type == "autoencoder":
+            fwd = _hip.FwdPlan(st.params, [(c, st.rows("test", c)) for c in range(C)], self.dims,
+                               want_sse=True, want_latent=False)
+            scores = fwd.sse_views()
+            adesc = _hip.auc_desc(scores, labels, aucs, 1.0 / self.dims.d_in)
+            p = dict(fwd=fwd, cen=None, ncen=0, scores=scores, test_lat=None)
+        else:
+            raise ValueError(f"unknown model_type {model_type!r}")
+        p["auc"] = torch.from_numpy(adesc.view(np.uint8).copy()).to(self.device)
+        p["aucs"] = aucs
+        p["labels"] = labels
+        self._eval_plans[model_type] = p
+        return p
+
+    def evaluate_launch(self, model_type: str) -> torch.Tensor:
+        """Enqueue the full AUC evaluation of every hosted client; returns the
+        device tensor of AUCs (float64 [C])."""
+        p = self._plan(model_type)
+        p["fwd"].run()
+        if p["cen"] is not None:
+            _hip.launch_cen(p["cen"], p["ncen"], self.device)
+        _hip.launch_auc(p["auc"], self.store.num_clients, self.device)
+        return p["aucs"]
+
+    def evaluate(self, model_type: str, metric: str = "AUC", keep_latents: bool = False):
+        from ..eval.evaluator import EvalResult, evaluate_clients
+
+        if metric != "AUC":
+            return evaluate_clients(self, list(range(self.store.num_clients)), model_type, metric, keep_latents)
+        aucs = self.evaluate_launch(model_type)
+        p = self._eval_plans[model_type]
+        vals = self._auc_fixup(self.fetch([aucs])[0], p["scores"], p["labels"])
+        latents = None
+        if keep_latents and p["test_lat"] is not None:
+            st = self.store
+            latents = [(l.detach().cpu().numpy().astype(np.float32), st.labels(c).astype(np.float32))
+                       for c, l in enumerate(p["test_lat"])]
+        return EvalResult(np.asarray(vals, dtype=np.float64), {}, latents)

@@ -17,7 +17,7 @@ import torch
 from ..models.layout import P_PAD, canonical_to_padded, padded_to_canonical
 from ..models.reference import functional_forward, functional_loss, unflatten
 from ..ops import _host
-from .base import Engine, TrainHParams, TrainResult
+from .base import Engine, TrainHandle, TrainHParams, TrainResult
 
 
 def _adam_update(p, g, m, v, step, hp: TrainHParams):
@@ -35,7 +35,13 @@ class TorchEngine(Engine):
     name = "torch"
 
     # -- training --------------------------------------------------------------
-    def train(self, local_ids: Sequence[int], hp: TrainHParams) -> TrainResult:
+    def train_launch(self, local_ids: Sequence[int], hp: TrainHParams) -> TrainHandle:
+        return TrainHandle(list(local_ids), [], self._train_eager(local_ids, hp))
+
+    def train_collect(self, handle: TrainHandle, host=None) -> TrainResult:
+        return handle.result
+
+    def _train_eager(self, local_ids: Sequence[int], hp: TrainHParams) -> TrainResult:
         st = self.store
         D = self.dims.d_in
         k = len(local_ids)

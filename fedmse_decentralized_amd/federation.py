@@ -36,6 +36,7 @@ from .engine import Engine, TrainHParams, make_engine
 from .eval.evaluator import evaluate_clients
 from .io import checkpoint as ckpt
 from .io import reports
+from .io.async_writer import AsyncWriter, snapshot_to_host
 from .models.layout import P_PAD, ModelDims
 from .models.reference import init_client_params
 from .parallel.comm import Comm, LoopbackComm
@@ -118,7 +119,8 @@ class Federation:
     def __init__(self, cfg: ExperimentConfig, model_type: str, update_type: str, run: int,
                  comm: Optional[Comm] = None, device: Optional[torch.device] = None,
                  early_stop: Optional[GlobalEarlyStop] = None, engine: Optional[Engine] = None,
-                 telemetry: Optional[Telemetry] = None, write_reports: bool = True):
+                 telemetry: Optional[Telemetry] = None, write_reports: bool = True,
+                 writer: Optional[AsyncWriter] = None):
         self.cfg = cfg
         self.model_type = model_type
         self.update_type = update_type
@@ -133,6 +135,7 @@ class Federation:
         self.round_idx = 0
         self.last_metrics: Optional[np.ndarray] = None
         self.latent_log: Dict[int, Dict[str, Tuple[np.ndarray, np.ndarray]]] = {}
+        self.writer = writer or _default_writer()
 
     # -- setup -------------------------------------------------------------------
     def setup(self):
@@ -185,109 +188,119 @@ class Federation:
         s, e = self.shard.bounds(self.comm.rank)
         return s <= cid < e
 
-    def _batch_mean_score(self, sse: torch.Tensor, bs: int) -> float:
-        """Mean over batches of per-batch MSE (`src/Trainer/client_trainer.py:226-241`)."""
-        D = self.dims.d_in
-        x = sse.detach().double().cpu().numpy()
-        n = x.shape[0]
-        tot, nb = 0.0, 0
-        for s in range(0, n, bs):
-            seg = x[s:s + bs]
-            tot += float(seg.sum() / (seg.shape[0] * D))
-            nb += 1
-        return tot / nb if nb else float("inf")
-
     def _gather_params(self, sources: Sequence[int], selected: Sequence[int]) -> torch.Tensor:
-        """Stack [len(sources), P] of the given clients' params (all ranks)."""
+        """Stack [len(sources), P] of the given clients' params (identical on all ranks).
+
+        World size 1: a device gather from the local store.  Otherwise every
+        rank packs its selected clients (selected order) into fixed slots and
+        one RCCL all-gather over xGMI delivers every rank's slots
+        ([world, slots, 9216] fp32) — the reference's "collect all selected
+        state_dicts" (`src/Trainer/client_trainer.py:306-315`) without a
+        single aggregator sink.
+        """
         st = self.engine.store
         if self.comm.world_size == 1:
-            idx = torch.tensor([self._loc(c) for c in sources], dtype=torch.long, device=st.params.device)
-            return st.params.index_select(0, idx)
-        # slot layout: each rank packs its selected clients in selected order
+            rows = [self._loc(c) for c in sources]
+            if rows == list(range(rows[0], rows[0] + len(rows))) if rows else False:
+                return st.params[rows[0]:rows[0] + len(rows)]
+            return torch.stack([st.params[r] for r in rows], 0)
         per_rank: Dict[int, List[int]] = {}
         for c in selected:
             per_rank.setdefault(self.shard.owner(c), []).append(c)
         slots = max(len(v) for v in per_rank.values())
         mine = per_rank.get(self.comm.rank, [])
         send = torch.zeros(slots, P_PAD, dtype=torch.float32, device=st.params.device)
-        if mine:
-            idx = torch.tensor([self._loc(c) for c in mine], dtype=torch.long, device=st.params.device)
-            send[:len(mine)] = st.params.index_select(0, idx)
-        allg = self.comm.all_gather(send)        # [world, slots, P]  (RCCL all-gather over xGMI)
-        rows = []
-        for c in sources:
-            r = self.shard.owner(c)
-            rows.append(allg[r, per_rank[r].index(c)])
-        return torch.stack(rows, 0)
+        for i, c in enumerate(mine):
+            send[i].copy_(st.params[self._loc(c)])
+        allg = self.comm.all_gather(send)        # [world, slots, P]
+        return torch.stack([allg[self.shard.owner(c), per_rank[self.shard.owner(c)].index(c)] for c in sources], 0)
+
+    def _write_checkpoints(self, res, local_sel: Sequence[int]) -> None:
+        """model.cpt (best-validation snapshot of this round's training) and
+        training_tracking.pkl per trained client, written by the background
+        writer from an asynchronous device->pinned copy."""
+        st = self.engine.store
+        snap, ev = snapshot_to_host(st.best)
+        dims = self.dims
+        for i, c in enumerate(local_sel):
+            d = self.save_dirs[c]
+            row = self._loc(c)
+            improved = res.best_epoch[i] >= 0
+            trk = list(res.tracking[i])
+
+            def job(d=d, row=row, improved=improved, trk=trk):
+                if improved:
+                    ckpt.save_model_cpt(d, snap[row], dims)
+                ckpt.save_tracking(d, trk)
+            self.writer.submit(job, ev)
 
     # -- one round ---------------------------------------------------------------
     def run_round(self) -> RoundResult:
         cfg, eng, st = self.cfg, self.engine, self.engine.store
         rnd = self.round_idx
         N = self.N
-        D = self.dims.d_in
-        log.info(f"Starting round {rnd + 1}/{cfg.num_rounds}")
+        info = log.isEnabledFor(logging.INFO)
+        if info:
+            log.info(f"Starting round {rnd + 1}/{cfg.num_rounds}")
 
         with self.tel.phase("select"):
             selected = select_clients(self.py_rng, N, cfg.num_participants)
             local_sel = [c for c in selected if self._mine(c)]
+            local_rows = [self._loc(c) for c in local_sel]
 
-        # ---------------- local training (all local selected clients, one launch)
+        # ---------------- local training of all local selected clients: one launch
         with self.tel.phase("train"):
-            for c in local_sel:
-                log.info(f"Training client {c + 1}...")
-            res = eng.train([self._loc(c) for c in local_sel], self.hp) if local_sel else None
-            epochs_local = {}
-            if res is not None:
-                for i, c in enumerate(local_sel):
-                    epochs_local[c] = int(res.epochs_run[i])
+            if info:
+                for c in local_sel:
+                    log.info(f"Training client {c + 1}...")
+            handle = eng.train_launch(local_rows, self.hp) if local_sel else None
+            if local_sel and cfg.malicious_clients:
+                for c in local_sel:
+                    if c in cfg.malicious_clients:   # fault injection: poisoned update
+                        st.params[self._loc(c)].mul_(cfg.malicious_scale)
+
+        # ---------------- vote scores (+ FedMSE dev MSE) of the local selected clients
+        with self.tel.phase("vote"):
+            need_dev = self.update_type == "mse_avg"
+            scores_dev = eng.vote_scores(local_rows, self.valid_all[selected[0]],
+                                         self.dev_set if need_dev else None, cfg.vote_batch_size)
+            # first host sync of the round: training results + scores
+            host = eng.fetch((handle.tensors if handle is not None else []) + [scores_dev])
+            scores_np = host[-1]
+            res = eng.train_collect(handle, host[:-1] if handle.tensors else None) if handle is not None else None
+        epochs_local: Dict[int, int] = {}
+        if res is not None:
+            for i, c in enumerate(local_sel):
+                epochs_local[c] = int(res.epochs_run[i])
+                if info:
                     for e, (tl, vl) in enumerate(res.tracking[i]):
                         log.info(f"[Client {c}] Epoch {e + 1} - Training loss: {tl} - Validating loss: {vl}")
                     log.info(f"Client {c + 1} training done!")
-                if cfg.malicious_clients:
-                    for i, c in enumerate(local_sel):
-                        if c in cfg.malicious_clients:   # fault injection: poisoned update
-                            st.params[self._loc(c)].mul_(cfg.malicious_scale)
-
-        with self.tel.phase("io"):
-            if res is not None and cfg.save_checkpoints:
-                for i, c in enumerate(local_sel):
-                    if res.best_epoch[i] >= 0:
-                        ckpt.save_model_cpt(self.save_dirs[c], st.best[self._loc(c)], self.dims)
-                    ckpt.save_tracking(self.save_dirs[c], res.tracking[i])
-
-        # ---------------- vote scores (+ FedMSE dev MSE), one all-reduce
+            if cfg.save_checkpoints:
+                with self.tel.phase("io"):
+                    self._write_checkpoints(res, local_sel)
         log.info("Starting voting for aggregator...")
-        with self.tel.phase("vote"):
-            vote_src = self.valid_all[selected[0]]
-            vs = eng.standardize_ddof1(vote_src)
-            items = [(self._loc(c), vs) for c in local_sel]
-            need_dev = self.update_type == "mse_avg"
-            if need_dev:
-                items += [(self._loc(c), self.dev_set) for c in local_sel]
-            sse, _ = eng.forward_rows(st.params, items, want_sse=True) if items else ([], None)
-            vec = torch.zeros(N, 3, dtype=torch.float64)
-            for i, c in enumerate(local_sel):
-                vec[c, 0] = self._batch_mean_score(sse[i], cfg.vote_batch_size)
-                if need_dev:
-                    s = sse[len(local_sel) + i]
-                    vec[c, 1] = float(s.double().sum().item()) / (s.shape[0] * D)
-                vec[c, 2] = epochs_local.get(c, 0)
+        vec = torch.zeros(N, 3, dtype=torch.float64)
+        for i, c in enumerate(local_sel):
+            vec[c, 0] = float(scores_np[i, 0])
+            vec[c, 1] = float(scores_np[i, 1]) if need_dev else 0.0
+            vec[c, 2] = epochs_local.get(c, 0)
         with self.tel.phase("comm"):
             vec = self.comm.all_reduce_sum(vec)
         with self.tel.phase("vote"):
             base_scores = {c: float(vec[c, 0]) for c in selected}
             dev_mse = {c: float(vec[c, 1]) for c in selected}
             epochs_all = {c: int(vec[c, 2]) for c in selected}
-            # torch-RNG replay: one iterator per train and per valid epoch loop
+            # torch-RNG replay (compat): one iterator per train and per valid epoch loop
             self.noise.iterators(2 * sum(epochs_all.values()))
             el = elect_aggregator(selected, base_scores, self.agg_counts, cfg.max_aggregation, self.noise,
-                                  log_enabled=log.isEnabledFor(logging.INFO))
+                                  log_enabled=info)
             aggregator = el.aggregator
 
         verification_results: List[Dict] = []
         if aggregator is not None:
-            log.info(f"Client {aggregator + 1} selected as aggregator")
+            if info:
+                log.info(f"Client {aggregator + 1} selected as aggregator")
             with self.tel.phase("aggregate"):
                 if self.update_type == "mse_avg":
                     for _ in selected:          # calculate_mse_score per client (weights unused, Q3)
@@ -299,41 +312,42 @@ class Federation:
                 agg = eng.weighted_sum(stack, [w for _, w in plan])
                 self.agg_counts[aggregator] += 1
                 if self._mine(aggregator):
-                    st.params[self._loc(aggregator)].copy_(agg)
+                    eng.adopt([self._loc(aggregator)], agg, anchor=False)
                 version = rnd
                 self.versions[version] = agg
             with self.tel.phase("verify"):
                 verification_results = self._verify_all(agg, version, aggregator, rnd)
             if self.write_reports:
-                with self.tel.phase("io"):
+                if info:
                     log.info("Verification results for this round:")
                     for r_ in verification_results:
                         log.info(f"Client {r_['client_id']}: {'Verified' if r_['is_verified'] else 'Rejected'} "
                                  f"(Rejected updates: {r_['rejected_updates']})")
-                    reports.append_verification(cfg, self.run, rnd, verification_results)
+                vr = verification_results
+                self.writer.submit(lambda vr=vr, rnd=rnd: reports.append_verification(cfg, self.run, rnd, vr))
         else:
             log.warning("No aggregator selected for this round")
 
-        # ---------------- evaluation of every client
+        # ---------------- evaluation of every hosted client (batched launches)
         log.info("Calculating metrics for all models...")
         with self.tel.phase("eval"):
-            er = evaluate_clients(eng, list(range(len(self.local))), self.model_type, cfg.metric,
-                                  keep_latents=cfg.save_latents)
+            er = eng.evaluate(self.model_type, cfg.metric, keep_latents=cfg.save_latents)
             vec = torch.zeros(N, dtype=torch.float64)
-            for i, c in enumerate(self.local):
-                vec[c] = float(er.metrics[i])
+            vec[self.local[0]:self.local[-1] + 1] = torch.from_numpy(np.asarray(er.metrics, dtype=np.float64))
         with self.tel.phase("comm"):
             vec = self.comm.all_reduce_sum(vec)
         metrics = vec.numpy().copy()
         self.noise.iterators(N * (2 if self.model_type == "hybrid" else 1))
-        for i in range(N):
-            log.info(f"Client {i + 1} {cfg.metric} score: {metrics[i]}")
+        if info:
+            for i in range(N):
+                log.info(f"Client {i + 1} {cfg.metric} score: {metrics[i]}")
         if cfg.save_latents and er.latents is not None:
             names = [self.clients[c].name for c in self.local]
             self.latent_log[rnd] = {n: l for n, l in zip(names, er.latents)}
-        with self.tel.phase("io"):
-            if self.write_reports:
-                reports.append_round_result(cfg, self.run, rnd, metrics, self.model_type, self.update_type)
+        if self.write_reports:
+            m_ = metrics.copy()
+            self.writer.submit(lambda m_=m_, rnd=rnd: reports.append_round_result(
+                cfg, self.run, rnd, m_, self.model_type, self.update_type))
         self.last_metrics = metrics
         stop = False
         if cfg.global_early_stop:
@@ -343,49 +357,43 @@ class Federation:
         return RoundResult(rnd, list(selected), aggregator, metrics, verification_results, epochs_all, stop, times)
 
     def _verify_all(self, agg: torch.Tensor, version: int, aggregator: int, rnd: int) -> List[Dict]:
-        cfg, eng, st = self.cfg, self.engine, self.engine.store
+        """Every receiver verifies the broadcast aggregate (all N clients but the
+        aggregator, Q14): one batched forward for the verification MSEs, one
+        drift launch, one host sync, then the accepted receivers adopt the
+        aggregate (and refresh their FedProx anchor) in one launch."""
+        cfg, eng = self.cfg, self.engine
         N = self.N
-        D = self.dims.d_in
         receivers = [c for c in self.local if c != aggregator]
-        # perf = 1 / (1 + MSE(V, model(V))) of the new aggregate (src/Trainer/model_verifier.py:86-99)
-        aggp = agg.unsqueeze(0)
         if cfg.verification_method == "dev":
-            datasets = {c: ("dev", self.dev_set) for c in receivers}
+            key_of = {c: "dev" for c in receivers}
+            data_of = {"dev": self.dev_set}
         elif cfg.compat == "reference":
             # every client verifies on the last-constructed client's validation set (Q4)
-            datasets = {c: ("vlast", self.valid_all[N - 1]) for c in receivers}
+            key_of = {c: "vlast" for c in receivers}
+            data_of = {"vlast": self.valid_all[N - 1]}
         else:
-            datasets = {c: (f"v{c}", self.valid_all[c]) for c in receivers}
-        keys = sorted({k for k, _ in datasets.values()})
-        keyed = {k: t for k, t in datasets.values()}
-        sse, _ = eng.forward_rows(aggp, [(0, keyed[k]) for k in keys], want_sse=True) if keys else ([], None)
-        perf = {}
-        for k, s in zip(keys, sse):
-            mse = float(s.double().sum().item()) / (s.shape[0] * D)
-            perf[k] = 1.0 / (1.0 + mse)
-        # drift against each receiver's previous received aggregate (grouped by version)
+            key_of = {c: f"v{c}" for c in receivers}
+            data_of = {f"v{c}": self.valid_all[c] for c in receivers}
+        keys = sorted(set(key_of.values()))
         need = sorted({self.vstate[c].history_version for c in receivers if self.vstate[c].history_version is not None})
-        drift = {}
-        if need:
-            hist = torch.stack([self.versions[v] for v in need], 0)
-            d = eng.param_drift(hist, agg).double().cpu().numpy()
-            drift = {v: float(x) for v, x in zip(need, d)}
+        hist = torch.stack([self.versions[v] for v in need], 0) if need else None
+        mse_t, drift_t = eng.verify_stats(agg, [data_of[k] for k in keys], hist)
+        mse_np, drift_np = eng.fetch([mse_t, drift_t])
+        perf = {k: 1.0 / (1.0 + float(m)) for k, m in zip(keys, mse_np)}   # 1 / (1 + MSE)
+        drift = {v: float(x) for v, x in zip(need, drift_np)}
         accept = []
         vec = torch.zeros(N, 2, dtype=torch.float64)
         for c in receivers:
             vs_ = self.vstate[c]
             dr = drift.get(vs_.history_version, 0.0) if vs_.history_version is not None else 0.0
-            dec = self.verifier.decide(c, vs_, version, perf[datasets[c][0]], dr, rnd)
+            dec = self.verifier.decide(c, vs_, version, perf[key_of[c]], dr, rnd)
             self.verifier.apply(c, vs_, dec)
             if dec.verified:
                 accept.append(c)
             vec[c, 0] = vs_.rejected_updates
             vec[c, 1] = 1.0
         if accept:
-            idx = torch.tensor([self._loc(c) for c in accept], dtype=torch.long, device=st.params.device)
-            rows = agg.unsqueeze(0).expand(len(accept), -1)
-            st.params.index_copy_(0, idx, rows)
-            st.anchor.index_copy_(0, idx, rows)      # previous_global_model = deepcopy(model)
+            eng.adopt([self._loc(c) for c in accept], agg, anchor=True)  # previous_global_model = deepcopy(model)
         self.noise.model_inits(N - 1)                # verifier builds a fresh model per call (Q16)
         # replicated bookkeeping: every non-aggregator received this version;
         # drop aggregate versions no client references any more
@@ -418,11 +426,12 @@ class Federation:
             if r.stop:
                 break
         if self.last_metrics is None:
-            er = evaluate_clients(self.engine, list(range(len(self.local))), self.model_type, cfg.metric)
+            er = self.engine.evaluate(self.model_type, cfg.metric)
             vec = torch.zeros(self.N, dtype=torch.float64)
             for i, c in enumerate(self.local):
                 vec[c] = float(er.metrics[i])
             self.last_metrics = self.comm.all_reduce_sum(vec).numpy()
+        self.writer.flush()
         if cfg.save_latents and self.latent_log:
             parts = self.comm.all_gather_object(self.latent_log)
             if self.comm.is_root:
@@ -476,6 +485,16 @@ class Federation:
         self.early.best, self.early.worse = float(s["early"][0]), int(s["early"][1])
         if s["last_metrics"].numel():
             self.last_metrics = s["last_metrics"].numpy()
+
+
+_WRITER: Optional[AsyncWriter] = None
+
+
+def _default_writer() -> AsyncWriter:
+    global _WRITER
+    if _WRITER is None:
+        _WRITER = AsyncWriter(enabled=True)
+    return _WRITER
 
 
 def _py_state_to_list(state):

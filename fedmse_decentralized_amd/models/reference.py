@@ -18,6 +18,8 @@ from __future__ import annotations
 from typing import List, Optional, Tuple
 
 import math
+import threading
+
 import torch
 from torch import nn
 
@@ -92,13 +94,18 @@ def init_client_params(num_clients: int, seed: int, dims: ModelDims = DEFAULT_DI
     (`utils/rng_replay.py`).
     """
     out = []
-    with torch.random.fork_rng(devices=[]):
+    with GLOBAL_RNG_LOCK, torch.random.fork_rng(devices=[]):
         torch.manual_seed(seed)
         for _ in range(num_clients):
             m = ReferenceSAE(dims, shrink_lambda=0.0)
             out.append(state_dict_to_canonical(m.state_dict(), dims))
         state = torch.get_rng_state()
     return torch.stack(out, 0), state
+
+
+# the global torch CPU generator is process state: serialise the code paths
+# that borrow it (in-process multi-rank tests run ranks on threads)
+GLOBAL_RNG_LOCK = threading.RLock()
 
 
 # ----------------------------------------------------------------------------

@@ -3,8 +3,13 @@
 The library has a plain C ABI (no torch headers); device memory is owned by
 torch tensors and passed as raw pointers together with the current HIP
 stream, so the kernels interleave correctly with torch work on that stream.
-Work lists (forward row blocks, CEN / AUC jobs) are small descriptor arrays
-built on the host and copied to the device per call.
+
+Work lists (forward row blocks, CEN / AUC / score jobs) are small descriptor
+arrays.  They are built with vectorised numpy and either
+* cached on the device for static work (every round evaluates the same
+  clients on the same buffers: ``Plan`` objects), or
+* staged through a pinned host ring and copied asynchronously on the stream
+  (``Uploader``) for per-round work — no pageable copies, no host syncs.
 
 Loading fails loudly: on a GPU box the HIP engine must run these kernels,
 never a silent PyTorch fallback.
@@ -13,7 +18,7 @@ from __future__ import annotations
 
 import ctypes
 import threading
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -36,6 +41,7 @@ AUC_DTYPE = np.dtype([
     ("score", "<u8"), ("label", "<u8"), ("out", "<u8"),
     ("n", "<i4"), ("score_is_f64", "<i4"), ("score_scale", "<f4"), ("pad", "<i4"),
 ])
+SEG_DTYPE = np.dtype([("sse", "<u8"), ("n", "<i4"), ("batch", "<i4"), ("out", "<u8")])
 
 FWD_ROWS_PER_BLOCK = 256   # 4 waves x 4 tiles of 16 rows
 
@@ -63,24 +69,30 @@ def lib():
         if _lib is None:
             path = build.HIP_LIB
             if not path.exists():
-                # build in-tree on first use (hipcc cross-compiles for gfx950)
-                build.build_hip()
+                build.build_hip()   # hipcc cross-compiles for gfx950 in-tree
             L = ctypes.CDLL(str(path))
             vp, i32 = ctypes.c_void_p, ctypes.c_int
-            L.fedmx_forward_rows.argtypes = [vp, i32, vp]
-            L.fedmx_weighted_sum.argtypes = [vp, vp, i32, i32, vp, vp]
-            L.fedmx_param_drift.argtypes = [vp, i32, vp, vp, vp, vp]
-            L.fedmx_standardize_ddof1.argtypes = [vp, i32, i32, vp, vp]
-            L.fedmx_cen_score.argtypes = [vp, i32, vp]
-            L.fedmx_auc.argtypes = [vp, i32, vp]
-            L.fedmx_train.argtypes = [ctypes.POINTER(TrainArgs), i32, vp]
-            L.fedmx_probe_mfma.argtypes = [vp, vp]
-            for f in ("fedmx_forward_rows", "fedmx_weighted_sum", "fedmx_param_drift", "fedmx_standardize_ddof1",
-                      "fedmx_cen_score", "fedmx_auc", "fedmx_train", "fedmx_probe_mfma"):
-                getattr(L, f).restype = ctypes.c_int
+            sig = {
+                "fedmx_forward_rows": [vp, i32, vp],
+                "fedmx_weighted_sum": [vp, vp, i32, i32, vp, vp],
+                "fedmx_param_drift": [vp, i32, vp, vp, vp, vp],
+                "fedmx_standardize_ddof1": [vp, i32, i32, vp, vp],
+                "fedmx_standardize_lds": [vp, i32, i32, vp, vp],
+                "fedmx_cen_score": [vp, i32, vp],
+                "fedmx_auc": [vp, i32, vp],
+                "fedmx_score_reduce": [vp, i32, i32, vp],
+                "fedmx_broadcast_rows": [vp, vp, vp, i32, vp, i32, vp],
+                "fedmx_train": [ctypes.POINTER(TrainArgs), i32, vp],
+                "fedmx_probe_mfma": [vp, vp],
+            }
+            for name, args in sig.items():
+                f = getattr(L, name)
+                f.argtypes = args
+                f.restype = ctypes.c_int
             assert L.fedmx_fwd_desc_size() == FWD_DTYPE.itemsize
             assert L.fedmx_cen_desc_size() == CEN_DTYPE.itemsize
             assert L.fedmx_auc_desc_size() == AUC_DTYPE.itemsize
+            assert L.fedmx_seg_desc_size() == SEG_DTYPE.itemsize
             assert L.fedmx_train_args_size() == ctypes.sizeof(TrainArgs)
             _lib = L
     return _lib
@@ -95,71 +107,273 @@ def _check(rc: int, what: str):
         raise RuntimeError(f"{what} failed with HIP error code {rc}")
 
 
-def _ptr(t: Optional[torch.Tensor]) -> int:
-    return 0 if t is None else t.data_ptr()
+# ---------------------------------------------------------------------------
+class Uploader:
+    """Pinned host ring -> device ring, asynchronous on the current stream.
+
+    A slot is reused only after the event recorded behind its copy has
+    completed, so the host never overwrites bytes a pending copy still reads;
+    device slots are consumed by kernels enqueued on the same stream before the
+    slot's next copy, so stream order protects them.
+    """
+
+    def __init__(self, device: torch.device, slot_bytes: int = 1 << 16, nslots: int = 64):
+        self.device = device
+        self.slot = slot_bytes
+        self.n = nslots
+        self.host = torch.empty(nslots * slot_bytes, dtype=torch.uint8).pin_memory()
+        self.host_np = self.host.numpy()
+        self.dev = torch.empty(nslots * slot_bytes, dtype=torch.uint8, device=device)
+        self.events: List[Optional[torch.cuda.Event]] = [None] * nslots
+        self.i = 0
+
+    def upload(self, *arrays: np.ndarray) -> List[int]:
+        """Copy one or more arrays in one transfer; returns their device addresses."""
+        blobs = [np.ascontiguousarray(a).view(np.uint8).reshape(-1) for a in arrays]
+        offs, tot = [], 0
+        for b in blobs:
+            offs.append(tot)
+            tot += (b.nbytes + 15) & ~15
+        if tot > self.slot:
+            t = torch.from_numpy(np.concatenate([np.pad(b, (0, ((b.nbytes + 15) & ~15) - b.nbytes)) for b in blobs]))
+            d = t.to(self.device)
+            self._keep = d   # large, rare: plain copy (kept alive until next call)
+            return [d.data_ptr() + o for o in offs]
+        s = self.i
+        self.i = (self.i + 1) % self.n
+        ev = self.events[s]
+        if ev is not None:
+            ev.synchronize()
+        base = s * self.slot
+        for b, o in zip(blobs, offs):
+            self.host_np[base + o: base + o + b.nbytes] = b
+        self.dev[base:base + tot].copy_(self.host[base:base + tot], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.events[s] = ev
+        ptr = self.dev.data_ptr() + base
+        return [ptr + o for o in offs]
 
 
-def _upload(arr: np.ndarray, device) -> torch.Tensor:
-    buf = torch.from_numpy(arr.view(np.uint8).reshape(-1))
-    return buf.to(device)
+_uploaders = {}
+
+
+def uploader(device: torch.device) -> Uploader:
+    key = (device.type, device.index)
+    u = _uploaders.get(key)
+    if u is None:
+        u = _uploaders[key] = Uploader(device)
+    return u
+
+
+class HostStage:
+    """Pinned staging for device->host readbacks: enqueue several async copies,
+    then one event wait (one host sync per protocol phase)."""
+
+    def __init__(self, device: torch.device, nbytes: int = 1 << 20):
+        self.device = device
+        self.buf = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+        self.off = 0
+        self.items = []
+
+    def add(self, t: torch.Tensor):
+        t = t.contiguous()
+        nb = t.numel() * t.element_size()
+        off = (self.off + 15) & ~15
+        if off + nb > self.buf.numel():
+            raise RuntimeError("HostStage overflow")
+        dst = self.buf[off:off + nb].view(t.dtype).view(t.shape)
+        dst.copy_(t, non_blocking=True)
+        self.off = off + nb
+        self.items.append(dst)
+        return len(self.items) - 1
+
+    def fetch(self) -> List[np.ndarray]:
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        ev.synchronize()
+        out = [x.numpy().copy() for x in self.items]
+        self.items = []
+        self.off = 0
+        return out
 
 
 # ---------------------------------------------------------------------------
+def build_fwd_desc(param_ptrs: np.ndarray, x_ptrs: np.ndarray, nrows: np.ndarray, sse_ptrs: np.ndarray,
+                   lat_ptrs: np.ndarray, dims) -> np.ndarray:
+    """Vectorised FwdDesc construction: split items into <=256-row blocks."""
+    nrows = np.asarray(nrows, dtype=np.int64)
+    nblk = (nrows + FWD_ROWS_PER_BLOCK - 1) // FWD_ROWS_PER_BLOCK
+    item = np.repeat(np.arange(len(nrows)), nblk)
+    first = np.repeat(np.cumsum(nblk) - nblk, nblk)
+    r0 = (np.arange(int(nblk.sum())) - first) * FWD_ROWS_PER_BLOCK
+    desc = np.zeros(len(item), dtype=FWD_DTYPE)
+    desc["params"] = param_ptrs[item]
+    desc["x"] = x_ptrs[item] + (4 * 128) * r0
+    desc["sse"] = np.where(sse_ptrs[item] != 0, sse_ptrs[item] + 4 * r0, 0)
+    desc["lat"] = np.where(lat_ptrs[item] != 0, lat_ptrs[item] + 4 * dims.latent * r0, 0)
+    desc["nrows"] = np.minimum(FWD_ROWS_PER_BLOCK, nrows[item] - r0)
+    desc["lat_stride"] = dims.latent
+    desc["d_in"] = dims.d_in
+    desc["latent"] = dims.latent
+    desc["hidden"] = dims.hidden
+    return desc
+
+
 def forward_rows(params: torch.Tensor, items, dims, want_sse=True, want_latent=False):
     """items: sequence of (param_row, x[n, DP]).  Returns (sse list, latent list)."""
     dev = params.device
-    n_items = len(items)
-    sizes = [int(x.shape[0]) for _, x in items]
-    tot = sum(sizes)
+    sizes = np.array([int(x.shape[0]) for _, x in items], dtype=np.int64)
+    tot = int(sizes.sum())
+    for _, x in items:
+        if x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != 128 or not x.is_contiguous() or x.device != dev:
+            raise ValueError("forward_rows expects contiguous float32 [n, 128] inputs on the params device")
     sse_all = torch.empty(tot, dtype=torch.float32, device=dev) if want_sse else None
     lat_all = torch.empty(tot, dims.latent, dtype=torch.float32, device=dev) if want_latent else None
-    nblocks = sum((n + FWD_ROWS_PER_BLOCK - 1) // FWD_ROWS_PER_BLOCK for n in sizes)
-    desc = np.zeros(nblocks, dtype=FWD_DTYPE)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
     P = params.shape[1]
-    base_p = params.data_ptr()
-    bi = 0
-    off = 0
-    for (row, x), n in zip(items, sizes):
-        if x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != 128 or not x.is_contiguous():
-            raise ValueError("forward_rows expects contiguous float32 [n, 128] inputs")
-        if x.device != dev:
-            raise ValueError("inputs must live on the params device")
-        for r0 in range(0, n, FWD_ROWS_PER_BLOCK):
-            nr = min(FWD_ROWS_PER_BLOCK, n - r0)
-            d = desc[bi]
-            d["params"] = base_p + 4 * P * int(row)
-            d["x"] = x.data_ptr() + 4 * 128 * r0
-            d["sse"] = (sse_all.data_ptr() + 4 * (off + r0)) if want_sse else 0
-            d["lat"] = (lat_all.data_ptr() + 4 * dims.latent * (off + r0)) if want_latent else 0
-            d["nrows"] = nr
-            d["lat_stride"] = dims.latent
-            d["d_in"] = dims.d_in
-            d["latent"] = dims.latent
-            d["hidden"] = dims.hidden
-            bi += 1
-        off += n
-    if nblocks:
-        dbuf = _upload(desc, dev)
-        _check(lib().fedmx_forward_rows(dbuf.data_ptr(), nblocks, _stream(dev)), "fedmx_forward_rows")
+    pptr = params.data_ptr() + 4 * P * np.array([int(r) for r, _ in items], dtype=np.int64)
+    xptr = np.array([x.data_ptr() for _, x in items], dtype=np.int64)
+    sptr = (sse_all.data_ptr() + 4 * offs) if want_sse else np.zeros(len(items), np.int64)
+    lptr = (lat_all.data_ptr() + 4 * dims.latent * offs) if want_latent else np.zeros(len(items), np.int64)
+    desc = build_fwd_desc(pptr, xptr, sizes, sptr, lptr, dims)
+    if len(desc):
+        (dptr,) = uploader(dev).upload(desc)
+        _check(lib().fedmx_forward_rows(dptr, len(desc), _stream(dev)), "fedmx_forward_rows")
     sse_l, lat_l = [], []
-    off = 0
-    for n in sizes:
+    for o, n in zip(offs, sizes):
         if want_sse:
-            sse_l.append(sse_all[off:off + n])
+            sse_l.append(sse_all[o:o + n])
         if want_latent:
-            lat_l.append(lat_all[off:off + n])
-        off += n
+            lat_l.append(lat_all[o:o + n])
     return sse_l, lat_l
 
 
-def weighted_sum(stack: torch.Tensor, weights: Sequence[float]) -> torch.Tensor:
+class FwdPlan:
+    """A cached forward launch over fixed (param row, buffer) items."""
+
+    def __init__(self, params: torch.Tensor, items, dims, want_sse: bool, want_latent: bool):
+        self.params = params
+        dev = params.device
+        self.device = dev
+        self.sizes = np.array([int(x.shape[0]) for _, x in items], dtype=np.int64)
+        tot = int(self.sizes.sum())
+        self.sse = torch.empty(tot, dtype=torch.float32, device=dev) if want_sse else None
+        self.lat = torch.empty(tot, dims.latent, dtype=torch.float32, device=dev) if want_latent else None
+        self.offs = np.concatenate([[0], np.cumsum(self.sizes)[:-1]]).astype(np.int64)
+        P = params.shape[1]
+        pptr = params.data_ptr() + 4 * P * np.array([int(r) for r, _ in items], dtype=np.int64)
+        xptr = np.array([x.data_ptr() for _, x in items], dtype=np.int64)
+        sptr = (self.sse.data_ptr() + 4 * self.offs) if want_sse else np.zeros(len(items), np.int64)
+        lptr = (self.lat.data_ptr() + 4 * dims.latent * self.offs) if want_latent else np.zeros(len(items), np.int64)
+        desc = build_fwd_desc(pptr, xptr, self.sizes, sptr, lptr, dims)
+        self.nblocks = len(desc)
+        self.desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+        self._keep = [x for _, x in items]
+
+    def run(self):
+        if self.nblocks:
+            _check(lib().fedmx_forward_rows(self.desc.data_ptr(), self.nblocks, _stream(self.device)),
+                   "fedmx_forward_rows")
+
+    def sse_views(self):
+        return [self.sse[o:o + n] for o, n in zip(self.offs, self.sizes)]
+
+    def lat_views(self):
+        return [self.lat[o:o + n] for o, n in zip(self.offs, self.sizes)]
+
+
+def cen_desc(train_lat, test_lat, out: torch.Tensor, latent: int) -> Tuple[np.ndarray, List[torch.Tensor]]:
+    n = len(train_lat)
+    desc = np.zeros(n, dtype=CEN_DTYPE)
+    views, off = [], 0
+    for i, (tr, te) in enumerate(zip(train_lat, test_lat)):
+        desc[i]["train_lat"] = tr.data_ptr()
+        desc[i]["test_lat"] = te.data_ptr()
+        desc[i]["out"] = out.data_ptr() + 8 * off
+        desc[i]["n_train"] = tr.shape[0]
+        desc[i]["n_test"] = te.shape[0]
+        desc[i]["latent"] = latent
+        desc[i]["stride"] = tr.stride(0)
+        views.append(out[off:off + te.shape[0]])
+        off += te.shape[0]
+    return desc, views
+
+
+def cen_scores(train_lat: Sequence[torch.Tensor], test_lat: Sequence[torch.Tensor], latent: int):
+    dev = train_lat[0].device
+    out_all = torch.empty(sum(int(t.shape[0]) for t in test_lat), dtype=torch.float64, device=dev)
+    desc, views = cen_desc(train_lat, test_lat, out_all, latent)
+    (dptr,) = uploader(dev).upload(desc)
+    _check(lib().fedmx_cen_score(dptr, len(desc), _stream(dev)), "fedmx_cen_score")
+    return views
+
+
+def auc_desc(scores, labels, out: torch.Tensor, f32_scale: float = 1.0) -> np.ndarray:
+    n = len(scores)
+    desc = np.zeros(n, dtype=AUC_DTYPE)
+    for i, (s, l) in enumerate(zip(scores, labels)):
+        if l.dtype != torch.int32:
+            raise ValueError("labels must be int32")
+        desc[i]["score"] = s.data_ptr()
+        desc[i]["label"] = l.data_ptr()
+        desc[i]["out"] = out.data_ptr() + 8 * i
+        desc[i]["n"] = s.shape[0]
+        desc[i]["score_is_f64"] = 1 if s.dtype == torch.float64 else 0
+        desc[i]["score_scale"] = f32_scale
+    return desc
+
+
+def auc(scores: Sequence[torch.Tensor], labels: Sequence[torch.Tensor], f32_scale: float = 1.0) -> torch.Tensor:
+    """Exact tie-aware ROC-AUC per (scores, labels) pair; float64 [n] on device.
+    -1 marks classes too large for the LDS sort (caller uses the host path)."""
+    dev = scores[0].device
+    out = torch.empty(len(scores), dtype=torch.float64, device=dev)
+    desc = auc_desc(scores, labels, out, f32_scale)
+    (dptr,) = uploader(dev).upload(desc)
+    _check(lib().fedmx_auc(dptr, len(desc), _stream(dev)), "fedmx_auc")
+    return out
+
+
+def launch_cen(desc_dev: torch.Tensor, n: int, device):
+    _check(lib().fedmx_cen_score(desc_dev.data_ptr(), n, _stream(device)), "fedmx_cen_score")
+
+
+def launch_auc(desc_dev: torch.Tensor, n: int, device):
+    _check(lib().fedmx_auc(desc_dev.data_ptr(), n, _stream(device)), "fedmx_auc")
+
+
+def score_reduce(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in: int) -> torch.Tensor:
+    """[len, 2] float64: (mean over batches of batch-MSE, overall MSE) per SSE segment."""
+    dev = sse_list[0].device
+    out = torch.empty(len(sse_list), 2, dtype=torch.float64, device=dev)
+    desc = np.zeros(len(sse_list), dtype=SEG_DTYPE)
+    desc["sse"] = [s.data_ptr() for s in sse_list]
+    desc["n"] = [int(s.shape[0]) for s in sse_list]
+    desc["batch"] = list(batch)
+    desc["out"] = out.data_ptr() + 16 * np.arange(len(sse_list), dtype=np.int64)
+    (dptr,) = uploader(dev).upload(desc)
+    _check(lib().fedmx_score_reduce(dptr, len(desc), d_in, _stream(dev)), "fedmx_score_reduce")
+    return out
+
+
+def broadcast_rows(dst0: torch.Tensor, dst1: Optional[torch.Tensor], rows: Sequence[int], src: torch.Tensor):
+    dev = dst0.device
+    if not len(rows):
+        return
+    (iptr,) = uploader(dev).upload(np.asarray(rows, dtype=np.int32))
+    _check(lib().fedmx_broadcast_rows(dst0.data_ptr(), 0 if dst1 is None else dst1.data_ptr(), iptr, len(rows),
+                                      src.data_ptr(), dst0.shape[1], _stream(dev)), "fedmx_broadcast_rows")
+
+
+def weighted_sum(stack: torch.Tensor, weights: Sequence[float], out: Optional[torch.Tensor] = None) -> torch.Tensor:
     dev = stack.device
     K, P = stack.shape
-    w = torch.tensor(np.asarray(weights, dtype=np.float32), device=dev)
-    out = torch.empty(P, dtype=torch.float32, device=dev)
+    (wptr,) = uploader(dev).upload(np.asarray(weights, dtype=np.float32))
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=dev)
     st = stack.contiguous()
-    _check(lib().fedmx_weighted_sum(st.data_ptr(), w.data_ptr(), K, P, out.data_ptr(), _stream(dev)),
-           "fedmx_weighted_sum")
+    _check(lib().fedmx_weighted_sum(st.data_ptr(), wptr, K, P, out.data_ptr(), _stream(dev)), "fedmx_weighted_sum")
     return out
 
 
@@ -174,70 +388,39 @@ def param_drift(hist: torch.Tensor, new: torch.Tensor, seg: torch.Tensor) -> tor
     return out
 
 
-def standardize_ddof1(x: torch.Tensor, d_in: int) -> torch.Tensor:
+def standardize_ddof1(x: torch.Tensor, d_in: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     dev = x.device
-    y = torch.empty_like(x)
-    _check(lib().fedmx_standardize_ddof1(x.data_ptr(), x.shape[0], d_in, y.data_ptr(), _stream(dev)),
-           "fedmx_standardize_ddof1")
+    y = torch.empty_like(x) if out is None else out
+    _check(lib().fedmx_standardize_lds(x.data_ptr(), x.shape[0], d_in, y.data_ptr(), _stream(dev)),
+           "fedmx_standardize_lds")
     return y
 
 
-def cen_scores(train_lat: Sequence[torch.Tensor], test_lat: Sequence[torch.Tensor], latent: int):
-    dev = train_lat[0].device
-    n = len(train_lat)
-    sizes = [int(t.shape[0]) for t in test_lat]
-    out_all = torch.empty(sum(sizes), dtype=torch.float64, device=dev)
-    desc = np.zeros(n, dtype=CEN_DTYPE)
-    off = 0
-    for i, (tr, te) in enumerate(zip(train_lat, test_lat)):
-        desc[i]["train_lat"] = tr.data_ptr()
-        desc[i]["test_lat"] = te.data_ptr()
-        desc[i]["out"] = out_all.data_ptr() + 8 * off
-        desc[i]["n_train"] = tr.shape[0]
-        desc[i]["n_test"] = te.shape[0]
-        desc[i]["latent"] = latent
-        desc[i]["stride"] = tr.stride(0)
-        off += te.shape[0]
-    dbuf = _upload(desc, dev)
-    _check(lib().fedmx_cen_score(dbuf.data_ptr(), n, _stream(dev)), "fedmx_cen_score")
-    res, off = [], 0
-    for s in sizes:
-        res.append(out_all[off:off + s])
-        off += s
-    return res
+class TrainBuffers:
+    """Persistent per-store device buffers for the training launch outputs."""
+
+    def __init__(self, store, max_epochs: int):
+        dev = store.params.device
+        C = store.num_clients
+        self.max_epochs = max_epochs
+        self.tracking = torch.empty(C, max_epochs, 2, dtype=torch.float64, device=dev)
+        self.epochs_run = torch.zeros(C, dtype=torch.int32, device=dev)
+        self.best_epoch = torch.zeros(C, dtype=torch.int32, device=dev)
+        self.train_off = torch.from_numpy(store.train_off).to(dev)
+        self.valid_off = torch.from_numpy(store.valid_off).to(dev)
 
 
-def auc(scores: Sequence[torch.Tensor], labels: Sequence[torch.Tensor], f32_scale: float = 1.0) -> torch.Tensor:
-    """Exact tie-aware ROC-AUC per (scores, labels) pair; returns float64 [n] on device.
-    A value of -1 marks sets too large for the LDS sort (caller falls back to host)."""
-    dev = scores[0].device
-    n = len(scores)
-    out = torch.empty(n, dtype=torch.float64, device=dev)
-    desc = np.zeros(n, dtype=AUC_DTYPE)
-    for i, (s, l) in enumerate(zip(scores, labels)):
-        if l.dtype != torch.int32:
-            raise ValueError("labels must be int32")
-        desc[i]["score"] = s.data_ptr()
-        desc[i]["label"] = l.data_ptr()
-        desc[i]["out"] = out.data_ptr() + 8 * i
-        desc[i]["n"] = s.shape[0]
-        desc[i]["score_is_f64"] = 1 if s.dtype == torch.float64 else 0
-        desc[i]["score_scale"] = f32_scale
-    dbuf = _upload(desc, dev)
-    _check(lib().fedmx_auc(dbuf.data_ptr(), n, _stream(dev)), "fedmx_auc")
-    return out
-
-
-def train(store, local_ids: Sequence[int], hp, dims):
+def train(store, local_ids: Sequence[int], hp, dims, bufs: Optional[TrainBuffers] = None):
+    """Launch the fused training kernel for store rows ``local_ids`` (async).
+    Returns (tracking[k, E, 2], epochs_run[k], best_epoch[k]) device views."""
     dev = store.params.device
     k = len(local_ids)
-    idx = torch.tensor(list(local_ids), dtype=torch.int32, device=dev)
-    tracking = torch.full((k, hp.epochs, 2), float("nan"), dtype=torch.float64, device=dev)
-    epochs_run = torch.zeros(k, dtype=torch.int32, device=dev)
-    best_epoch = torch.full((k,), -1, dtype=torch.int32, device=dev)
-    if not hasattr(store, "_train_off_dev"):
-        store._train_off_dev = torch.from_numpy(store.train_off).to(dev)
-        store._valid_off_dev = torch.from_numpy(store.valid_off).to(dev)
+    if bufs is None:
+        bufs = getattr(store, "_train_bufs", None)
+    if bufs is None or bufs.max_epochs < hp.epochs or bufs.tracking.shape[0] < k:
+        bufs = TrainBuffers(store, max(hp.epochs, 1))
+        store._train_bufs = bufs
+    (iptr,) = uploader(dev).upload(np.asarray(local_ids, dtype=np.int32))
     a = TrainArgs()
     a.params = store.params.data_ptr()
     a.adam_m = store.adam_m.data_ptr()
@@ -246,13 +429,15 @@ def train(store, local_ids: Sequence[int], hp, dims):
     a.best = store.best.data_ptr()
     a.adam_step = store.adam_step.data_ptr()
     a.train_x = store.train.data_ptr()
-    a.train_off = store._train_off_dev.data_ptr()
+    a.train_off = bufs.train_off.data_ptr()
     a.valid_x = store.valid.data_ptr()
-    a.valid_off = store._valid_off_dev.data_ptr()
-    a.client_idx = idx.data_ptr()
-    a.tracking = tracking.data_ptr()
-    a.epochs_run = epochs_run.data_ptr()
-    a.best_epoch = best_epoch.data_ptr()
+    a.valid_off = bufs.valid_off.data_ptr()
+    a.client_idx = iptr
+    # tracking rows are written with stride hp.epochs
+    trk = bufs.tracking.view(-1)[:k * hp.epochs * 2].view(k, hp.epochs, 2)
+    a.tracking = trk.data_ptr()
+    a.epochs_run = bufs.epochs_run.data_ptr()
+    a.best_epoch = bufs.best_epoch.data_ptr()
     a.epochs = hp.epochs
     a.batch = hp.batch_size
     a.patience = hp.patience
@@ -263,13 +448,11 @@ def train(store, local_ids: Sequence[int], hp, dims):
     if rc == -2:
         raise ValueError(f"fused training kernel supports batch sizes 1..16, got {hp.batch_size}")
     _check(rc, "fedmx_train")
-    return tracking, epochs_run, best_epoch, idx
+    return trk, bufs.epochs_run[:k], bufs.best_epoch[:k]
 
 
 def probe_mfma(device) -> np.ndarray:
-    """Runs one v_mfma_f32_16x16x4_f32 on known operands: returns D [16,16]
-    computed from A[i][k] = i + 100k, B[k][j] = 1000k + j (asymmetric)."""
+    """One v_mfma_f32_16x16x4_f32 on A[i][k] = i + 100k, B[k][j] = 1000k + j."""
     out = torch.zeros(16 * 16, dtype=torch.float32, device=device)
-    dummy = torch.zeros(1, dtype=torch.float32, device=device)
     _check(lib().fedmx_probe_mfma(out.data_ptr(), _stream(device)), "fedmx_probe_mfma")
     return out.view(16, 16).cpu().numpy()

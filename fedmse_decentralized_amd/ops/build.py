@@ -78,8 +78,11 @@ def build_hip(force: bool = False, verbose: bool = False, extra_flags=()) -> Pat
         return HIP_LIB
     LIBDIR.mkdir(parents=True, exist_ok=True)
     tmp = HIP_LIB.with_suffix(".so.tmp")
+    # -ffp-contract=off: separately rounded mul/add like the torch ops the kernels
+    # reproduce (aggregation sums are then bit-identical to the reference order)
     cmd = [hipcc_path(), f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-munsafe-fp-atomics", f"-I{CSRC / 'hip'}", *extra_flags, *map(str, srcs), "-o", str(tmp)]
+           "-ffp-contract=off", "-munsafe-fp-atomics", f"-I{CSRC / 'hip'}", *extra_flags, *map(str, srcs),
+           "-o", str(tmp)]
     out = _run(cmd)
     os.replace(tmp, HIP_LIB)
     if verbose:

@@ -27,55 +27,77 @@ struct CenDesc {
 };
 static_assert(sizeof(CenDesc) == 40, "CenDesc layout is shared with Python");
 
+// All latent dimensions are reduced together: one wave-shuffle + LDS pass per
+// statistic (3 block reductions instead of 3 per dimension).
+__device__ __forceinline__ void block_sum_vec(double* v, int m, double* s_red /*[4][ZP]*/) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < ZP; ++j) {
+    if (j >= m) break;
+    double x = v[j];
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    if (lane == 0) s_red[wv * ZP + j] = x;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ZP; ++j)
+    if (j < m) v[j] = s_red[j] + s_red[ZP + j] + s_red[2 * ZP + j] + s_red[3 * ZP + j];
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void cen_score_kernel(const CenDesc* __restrict__ descs) {
   const CenDesc d = descs[blockIdx.x];
-  __shared__ double red[256];
+  __shared__ double s_red[4 * ZP];
   __shared__ double s_mean[ZP];
   __shared__ double s_scale[ZP];
   const int tid = threadIdx.x;
-  for (int j = 0; j < d.latent; ++j) {
-    // mean (float64 sum of float32 values)
-    double s = 0.0;
-    for (int r = tid; r < d.n_train; r += blockDim.x) s += (double)d.train_lat[(size_t)r * d.stride + j];
-    red[tid] = s;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (tid < o) red[tid] += red[tid + o];
-      __syncthreads();
+  const int m = d.latent;
+  double acc[ZP], acc2[ZP];
+  // mean (float64 sums of float32 values)
+#pragma unroll
+  for (int j = 0; j < ZP; ++j) acc[j] = 0.0;
+  for (int r = tid; r < d.n_train; r += blockDim.x) {
+    const float* row = d.train_lat + (size_t)r * d.stride;
+#pragma unroll
+    for (int j = 0; j < ZP; ++j)
+      if (j < m) acc[j] += (double)row[j];
+  }
+  block_sum_vec(acc, m, s_red);
+  double mean[ZP];
+#pragma unroll
+  for (int j = 0; j < ZP; ++j) mean[j] = (j < m) ? acc[j] / d.n_train : 0.0;
+  // corrected two-pass variance: (sum (x-m)^2 - (sum (x-m))^2 / n) / n
+#pragma unroll
+  for (int j = 0; j < ZP; ++j) {
+    acc[j] = 0.0;
+    acc2[j] = 0.0;
+  }
+  for (int r = tid; r < d.n_train; r += blockDim.x) {
+    const float* row = d.train_lat + (size_t)r * d.stride;
+#pragma unroll
+    for (int j = 0; j < ZP; ++j) {
+      if (j < m) {
+        const double df = (double)row[j] - mean[j];
+        acc[j] += df;
+        acc2[j] += df * df;
+      }
     }
-    const double mean = red[0] / d.n_train;
-    __syncthreads();
-    // corrected two-pass variance: (sum (x-m)^2 - (sum (x-m))^2 / n) / n
-    double a = 0.0, b = 0.0;
-    for (int r = tid; r < d.n_train; r += blockDim.x) {
-      const double df = (double)d.train_lat[(size_t)r * d.stride + j] - mean;
-      a += df;
-      b += df * df;
-    }
-    red[tid] = a;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (tid < o) red[tid] += red[tid + o];
-      __syncthreads();
-    }
-    const double corr = red[0];
-    __syncthreads();
-    red[tid] = b;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (tid < o) red[tid] += red[tid + o];
-      __syncthreads();
-    }
-    if (tid == 0) {
-      const double n = (double)d.n_train;
-      const double var = (red[0] - corr * corr / n) / n;
+  }
+  block_sum_vec(acc, m, s_red);
+  block_sum_vec(acc2, m, s_red);
+  if (tid == 0) {
+    const double n = (double)d.n_train;
+#pragma unroll
+    for (int j = 0; j < ZP; ++j) {
+      if (j >= m) break;
+      const double var = (acc2[j] - acc[j] * acc[j] / n) / n;
       const double eps = DBL_EPSILON;
-      const double upper = n * eps * var + (n * mean * eps) * (n * mean * eps);
-      s_mean[j] = mean;
+      const double upper = n * eps * var + (n * mean[j] * eps) * (n * mean[j] * eps);
+      s_mean[j] = mean[j];
       s_scale[j] = (var <= upper) ? 1.0 : sqrt(var);
     }
-    __syncthreads();
   }
+  __syncthreads();
   for (int r = tid; r < d.n_test; r += blockDim.x) {
     double acc = 0.0;
     for (int j = 0; j < d.latent; ++j) {

@@ -15,9 +15,12 @@
 //     epilogue.  Layer 1 is K-split by the same column block (partial sums
 //     reduced through LDS, barrier #1); layer 4 output / dY rows by the same
 //     row block; dH3 = W4a^T dY is K-split again (barrier #2).
-//   * The 2 KB layers W2a / W3a and their gradients are computed redundantly
-//     (bit-identically) by every wave, each keeping a private copy, so they
-//     need no synchronisation.
+//   * The small layers W2a [16x32] / W3a [32x16] are two 16x16 gradient tiles
+//     each; wave 0/1 own the two W3a tiles, wave 2/3 the two W2a tiles (Adam
+//     state in registers).  Their forward/backward-data products are computed
+//     redundantly by every wave from one shared LDS master, which owners
+//     update after barrier #2 and readers re-read after barrier #1 of the next
+//     step, so no extra synchronisation is needed.
 //   * Per training step: 2 workgroup barriers; per validation batch: 1.
 //   * Global memory is touched only to stream the batches (prefetched one step
 //     ahead) and, through LDS staging with coalesced 16-byte accesses, to load
@@ -26,6 +29,10 @@
 // (reference default 12, src/main.py:52); padded batch columns and padded
 // features are masked out of the loss and every gradient.
 #include "fedmx_common.h"
+
+#ifndef FEDMX_EXACT_ADAM
+#define FEDMX_EXACT_ADAM 0
+#endif
 
 namespace fedmx {
 
@@ -49,87 +56,93 @@ struct TrainArgs {
 };
 
 struct AdamStep {
-  float one_m_b1, b2, one_m_b2, bc2s, eps, neg_step_size, two_mu;
+  float one_m_b1, b2, one_m_b2, inv_bc2s, bc2s, eps, neg_step_size, two_mu;
 };
 
+// torch.optim.Adam single-tensor update (no weight decay / amsgrad):
+//   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2)
+//   p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1)
+// Default build: hardware sqrt / reciprocal (<= 1 ulp each) instead of the
+// IEEE division sequences — 4x fewer instructions on the critical path.
 template <bool PROX>
 __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float a, float grad, const AdamStep& K,
                                             float& prox_acc) {
   float gr = grad;
   if (PROX) {
-    const float dp = __fsub_rn(p, a);
-    prox_acc = __fmaf_rn(dp, dp, prox_acc);
-    gr = __fadd_rn(gr, __fmul_rn(K.two_mu, dp));
+    const float dp = p - a;
+    prox_acc += dp * dp;
+    gr = gr + K.two_mu * dp;
   }
-  // m.lerp_(g, 1-b1);  v.mul_(b2).addcmul_(g, g, 1-b2)
-  m = __fadd_rn(m, __fmul_rn(K.one_m_b1, __fsub_rn(gr, m)));
-  v = __fadd_rn(__fmul_rn(v, K.b2), __fmul_rn(__fmul_rn(K.one_m_b2, gr), gr));
-  // denom = sqrt(v) / sqrt(bc2) + eps;  p.addcdiv_(m, denom, -step_size)
-  const float den = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), K.bc2s), K.eps);
-  p = __fadd_rn(p, __fmul_rn(K.neg_step_size, __fdiv_rn(m, den)));
+  m = m + K.one_m_b1 * (gr - m);
+  v = v * K.b2 + (K.one_m_b2 * gr) * gr;
+#if FEDMX_EXACT_ADAM
+  const float den = __fsqrt_rn(v) / K.bc2s + K.eps;
+  p = p + K.neg_step_size * (m / den);
+#else
+  const float den = __builtin_amdgcn_sqrtf(v) * K.inv_bc2s + K.eps;
+  p = p + K.neg_step_size * (m * __builtin_amdgcn_rcpf(den));
+#endif
 }
 
 // LDS plan (floats); total < 160 KiB -> one workgroup per CU.
 constexpr int L_W1 = HP * S_W1;          // 4224  shared, column block per wave
 constexpr int L_W4 = DP * S_W4;          // 4608  shared, row block per wave
-constexpr int L_W2 = ZP * S_W2;          // 576   per-wave private copy
-constexpr int L_W3 = HP * S_W3;          // 640   per-wave private copy
+constexpr int L_W2 = ZP * S_W2;          // 576   shared master
+constexpr int L_W3 = HP * S_W3;          // 640   shared master
 constexpr int L_RED = 4 * 2 * 64 * 4;    // 2048  one partial-sum exchange buffer
 constexpr int L_T32 = 32 * S_T;          // 640   [32 features][batch] transpose tile
 constexpr int L_T16 = 16 * S_T;          // 320
 constexpr int L_SCR = 4 * L_T32 + 2 * L_T16;  // 3200 per wave
-constexpr int L_TOTAL = L_W1 + L_W4 + 4 * (L_W2 + L_W3) + 3 * L_RED + 4 * L_SCR + 64;
+constexpr int L_TOTAL = L_W1 + L_W4 + L_W2 + L_W3 + 3 * L_RED + 4 * L_SCR + 64;
 
-// Parameter state owned by one lane (MFMA D layouts):
+// Per-lane state of the big owned blocks (MFMA D layouts):
 //   q1[t][v][r] = W1a[16t+4g+r][32w+16v+c]      q4[v][t][r] = W4a[32w+16v+4g+r][16t+c]
-//   q2[t][r]    = W2a[4g+r][16t+c]              q3[t][r]    = W3a[16t+4g+r][c]
-struct Owned {
+// plus the owned small tile o[r]:
+//   w<2 : W3a[16w+4g+r][c]                      w>=2: W2a[4g+r][16(w-2)+c]
+struct Slab {
   float q1[2][2][4];
   float q4[2][2][4];
-  float q2[2][4];
-  float q3[2][4];
+  float o[4];
 };
 
-struct LdsPtrs {
+struct Lane {
   float* w1;   // sW1 + 4g*S_W1 + 32w + c       (D-layout element base)
   float* w4;   // sW4 + (32w+4g)*S_W4 + c
-  float* w2;   // own W2 copy + 4g*S_W2 + c
-  float* w3;   // own W3 copy + 4g*S_W3 + c
+  float* own;  // owned small tile base (stride own_stride per r)
+  int own_stride;
 };
 
-__device__ __forceinline__ void owned_to_lds(const Owned& o, const LdsPtrs& L) {
+__device__ __forceinline__ void slab_to_lds(const Slab& o, const Lane& L) {
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int v = 0; v < 2; ++v) {
         L.w1[(16 * t + r) * S_W1 + 16 * v] = o.q1[t][v][r];
         L.w4[(16 * v + r) * S_W4 + 16 * t] = o.q4[v][t][r];
       }
-      L.w2[r * S_W2 + 16 * t] = o.q2[t][r];
-      L.w3[(16 * t + r) * S_W3] = o.q3[t][r];
-    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) L.own[r * L.own_stride] = o.o[r];
 }
 
-__device__ __forceinline__ void lds_to_owned(Owned& o, const LdsPtrs& L) {
+__device__ __forceinline__ void lds_to_slab(Slab& o, const Lane& L) {
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int v = 0; v < 2; ++v) {
         o.q1[t][v][r] = L.w1[(16 * t + r) * S_W1 + 16 * v];
         o.q4[v][t][r] = L.w4[(16 * v + r) * S_W4 + 16 * t];
       }
-      o.q2[t][r] = L.w2[r * S_W2 + 16 * t];
-      o.q3[t][r] = L.w3[(16 * t + r) * S_W3];
-    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o.o[r] = L.own[r * L.own_stride];
 }
 
-// dense global [P_PAD] -> LDS masters (W2a/W3a into every wave's copy)
+// dense global [P_PAD] <-> LDS masters
 __device__ __forceinline__ void global_to_masters(const float* __restrict__ src, float* sW1, float* sW4,
-                                                  float* sW23) {
+                                                  float* sW2, float* sW3) {
   const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
   for (int i = threadIdx.x; i < P_PAD / 4; i += 256) {
     const f32x4 val = s4[i];
@@ -138,13 +151,10 @@ __device__ __forceinline__ void global_to_masters(const float* __restrict__ src,
       lds_write4(&sW1[(e / DP) * S_W1 + (e % DP)], val);
     } else if (e < OFF_W3) {
       e -= OFF_W2;
-#pragma unroll
-      for (int ww = 0; ww < 4; ++ww) lds_write4(&sW23[ww * (L_W2 + L_W3) + (e / HP) * S_W2 + (e % HP)], val);
+      lds_write4(&sW2[(e / HP) * S_W2 + (e % HP)], val);
     } else if (e < OFF_W4) {
       e -= OFF_W3;
-#pragma unroll
-      for (int ww = 0; ww < 4; ++ww)
-        lds_write4(&sW23[ww * (L_W2 + L_W3) + L_W2 + (e / ZP) * S_W3 + (e % ZP)], val);
+      lds_write4(&sW3[(e / ZP) * S_W3 + (e % ZP)], val);
     } else {
       e -= OFF_W4;
       lds_write4(&sW4[(e / HP) * S_W4 + (e % HP)], val);
@@ -152,9 +162,8 @@ __device__ __forceinline__ void global_to_masters(const float* __restrict__ src,
   }
 }
 
-// LDS masters -> dense global [P_PAD] (W2a/W3a from wave 0's copy)
 __device__ __forceinline__ void masters_to_global(float* __restrict__ dst, const float* sW1, const float* sW4,
-                                                  const float* sW23) {
+                                                  const float* sW2, const float* sW3) {
   f32x4* d4 = reinterpret_cast<f32x4*>(dst);
   for (int i = threadIdx.x; i < P_PAD / 4; i += 256) {
     int e = i * 4;
@@ -163,10 +172,10 @@ __device__ __forceinline__ void masters_to_global(float* __restrict__ dst, const
       val = lds_read4(&sW1[(e / DP) * S_W1 + (e % DP)]);
     } else if (e < OFF_W3) {
       e -= OFF_W2;
-      val = lds_read4(&sW23[(e / HP) * S_W2 + (e % HP)]);
+      val = lds_read4(&sW2[(e / HP) * S_W2 + (e % HP)]);
     } else if (e < OFF_W4) {
       e -= OFF_W3;
-      val = lds_read4(&sW23[L_W2 + (e / ZP) * S_W3 + (e % ZP)]);
+      val = lds_read4(&sW3[(e / ZP) * S_W3 + (e % ZP)]);
     } else {
       e -= OFF_W4;
       val = lds_read4(&sW4[(e / HP) * S_W4 + (e % HP)]);
@@ -184,10 +193,9 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   const int g = lane >> 4;
   float* const sW1 = lds;
   float* const sW4 = sW1 + L_W1;
-  float* const sW23 = sW4 + L_W4;                  // 4 x (W2 copy, W3 copy)
-  float* const sW2 = sW23 + w * (L_W2 + L_W3);
+  float* const sW2 = sW4 + L_W4;
   float* const sW3 = sW2 + L_W2;
-  float* const sRedH1 = sW23 + 4 * (L_W2 + L_W3);  // two buffers (parity)
+  float* const sRedH1 = sW3 + L_W3;               // two buffers (parity)
   float* const sRedDH3 = sRedH1 + 2 * L_RED;
   float* const scr = sRedDH3 + L_RED + w * L_SCR;
   float* const sXT = scr;                // X^T own 32 columns      [32][S_T]
@@ -198,16 +206,22 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   float* const sDZT = sZT + L_T16;       // dZ^T                    [16][S_T]
   double* const sLoss = reinterpret_cast<double*>(sRedDH3 + L_RED + 4 * L_SCR);  // [4][4] doubles
 
-  // per-lane bases: D-layout element (write) and A/B-operand (read) addressing
-  LdsPtrs L;
+  Lane L;
   L.w1 = sW1 + 4 * g * S_W1 + 32 * w + c;
   L.w4 = sW4 + (32 * w + 4 * g) * S_W4 + c;
-  L.w2 = sW2 + 4 * g * S_W2 + c;
-  L.w3 = sW3 + 4 * g * S_W3 + c;
+  if (w < 2) {
+    L.own = sW3 + (16 * w + 4 * g) * S_W3 + c;
+    L.own_stride = S_W3;
+  } else {
+    L.own = sW2 + 4 * g * S_W2 + 16 * (w - 2) + c;
+    L.own_stride = S_W2;
+  }
   const float* const a1p = sW1 + c * S_W1 + 32 * w + 4 * g;   // + 16t*S_W1 + 16v
   const float* const a4p = sW4 + (32 * w + c) * S_W4 + 4 * g;  // + 16v*S_W4 + 16t
   const float* const a2p = sW2 + c * S_W2 + 4 * g;             // + 16t
   const float* const a3p = sW3 + c * S_W3 + 4 * g;             // + 16t*S_W3
+  const float* const d2p = sW2 + 4 * g * S_W2 + c;             // W2a[4g+r][16t+c]  (+ r*S_W2 + 16t)
+  const float* const d3p = sW3 + 4 * g * S_W3 + c;             // W3a[16t+4g+r][c]  (+ (16t+r)*S_W3)
   const int tw = 4 * g * S_T + c;   // transpose write: [feature 4g+r (+16v)][b=c]
   const int tr = c * S_T + 4 * g;   // transpose read : [feature c (+16v)][b=4g..4g+3]
   float* const redw = sRedDH3 + (w * 2) * 256 + lane * 4;  // own dH3 partial slot (+ t*256)
@@ -221,24 +235,24 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   const int d_in = A.d_in, hidden = A.hidden, latent = A.latent;
 
   // ---- load client state: global -> LDS masters -> owned registers ----------
-  Owned P, M, V, AN;
-  global_to_masters(Mg, sW1, sW4, sW23);
+  Slab P, M, V, AN;
+  global_to_masters(Mg, sW1, sW4, sW2, sW3);
   __syncthreads();
-  lds_to_owned(M, L);
+  lds_to_slab(M, L);
   __syncthreads();
-  global_to_masters(Vg, sW1, sW4, sW23);
+  global_to_masters(Vg, sW1, sW4, sW2, sW3);
   __syncthreads();
-  lds_to_owned(V, L);
+  lds_to_slab(V, L);
   __syncthreads();
   if (PROX) {
-    global_to_masters(A.anchor + (size_t)cid * P_PAD, sW1, sW4, sW23);
+    global_to_masters(A.anchor + (size_t)cid * P_PAD, sW1, sW4, sW2, sW3);
     __syncthreads();
-    lds_to_owned(AN, L);
+    lds_to_slab(AN, L);
     __syncthreads();
   }
-  global_to_masters(Pg, sW1, sW4, sW23);
+  global_to_masters(Pg, sW1, sW4, sW2, sW3);
   __syncthreads();
-  lds_to_owned(P, L);   // masters keep the live parameters from here on
+  lds_to_slab(P, L);   // masters keep the live parameters from here on
 
   const int B = A.batch;
   const float* const Xtr = A.train_x + (size_t)A.train_off[cid] * DP;
@@ -251,6 +265,15 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   int parity = 0;
   const bool bias_lane = (w == 3 && g == 3);  // holds X column DP-1 (= 32*3 + 16 + 4*3 + 3)
   const int xcol = 32 * w + 4 * g;
+  const float lam = A.lambda;
+  const float inv_d = 1.0f / (float)d_in;
+  // loop-invariant feature masks as 0/1 multipliers (own 8 feature rows)
+  float fm0[4], fm1[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    fm0[r] = (xcol + r < d_in) ? 1.f : 0.f;
+    fm1[r] = (xcol + 16 + r < d_in) ? 1.f : 0.f;
+  }
 
   auto load_x = [&](const float* X, int row0, int bcur, f32x4& x0, f32x4& x1) {
     const bool ok = c < bcur;
@@ -266,16 +289,24 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   auto forward = [&](const f32x4& x0, const f32x4& x1, int bcur, f32x4 (&h1)[2], f32x4& z, f32x4& zb,
                      f32x4 (&h3)[2], f32x4 (&y)[2], float& norm_c, double& lacc) {
     float* red = sRedH1 + parity * L_RED;
+    {
+      f32x4 acc0 = zero4(), acc1 = zero4();
+      const f32x4 a00 = lds_read4(a1p);
+      const f32x4 a01 = lds_read4(a1p + 16);
+      const f32x4 a10 = lds_read4(a1p + 16 * S_W1);
+      const f32x4 a11 = lds_read4(a1p + 16 * S_W1 + 16);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      f32x4 acc = zero4();
-      const f32x4 a0 = lds_read4(a1p + 16 * t * S_W1);
-      const f32x4 a1 = lds_read4(a1p + 16 * t * S_W1 + 16);
+      for (int j = 0; j < 4; ++j) {
+        acc0 = mfma16(a00[j], x0[j], acc0);
+        acc1 = mfma16(a10[j], x0[j], acc1);
+      }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc = mfma16(a0[j], x0[j], acc);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc = mfma16(a1[j], x1[j], acc);
-      lds_write4(red + (w * 2 + t) * 256 + lane * 4, acc);
+      for (int j = 0; j < 4; ++j) {
+        acc0 = mfma16(a01[j], x1[j], acc0);
+        acc1 = mfma16(a11[j], x1[j], acc1);
+      }
+      lds_write4(red + (w * 2 + 0) * 256 + lane * 4, acc0);
+      lds_write4(red + (w * 2 + 1) * 256 + lane * 4, acc1);
     }
     __syncthreads();  // barrier #1
 #pragma unroll
@@ -285,7 +316,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       for (int ww = 1; ww < 4; ++ww) {
         const f32x4 o = lds_read4(red + (ww * 2 + t) * 256 + lane * 4);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s[r] = __fadd_rn(s[r], o[r]);
+        for (int r = 0; r < 4; ++r) s[r] = s[r] + o[r];
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -297,55 +328,71 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
     }
     parity ^= 1;
     z = zero4();
+    {
+      const f32x4 a0 = lds_read4(a2p);
+      const f32x4 a1 = lds_read4(a2p + 16);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const f32x4 a = lds_read4(a2p + 16 * t);
+      for (int s = 0; s < 4; ++s) z = mfma16(a0[s], h1[0][s], z);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) z = mfma16(a[s], h1[t][s], z);
+      for (int s = 0; s < 4; ++s) z = mfma16(a1[s], h1[1][s], z);
     }
     zb = z;
     if (g == 3) zb[3] = 1.f;
+    {
+      f32x4 acc0 = zero4(), acc1 = zero4();
+      const f32x4 a0 = lds_read4(a3p);
+      const f32x4 a1 = lds_read4(a3p + 16 * S_W3);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      f32x4 acc = zero4();
-      const f32x4 a = lds_read4(a3p + 16 * t * S_W3);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc = mfma16(a[s], zb[s], acc);
+      for (int s = 0; s < 4; ++s) {
+        acc0 = mfma16(a0[s], zb[s], acc0);
+        acc1 = mfma16(a1[s], zb[s], acc1);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float vv = fmaxf(acc[r], 0.f);
-        if (16 * t + 4 * g + r == HP - 1) vv = 1.f;
-        acc[r] = vv;
+        float v0 = fmaxf(acc0[r], 0.f), v1 = fmaxf(acc1[r], 0.f);
+        if (16 + 4 * g + r == HP - 1) v1 = 1.f;
+        acc0[r] = v0;
+        acc1[r] = v1;
       }
-      h3[t] = acc;
+      h3[0] = acc0;
+      h3[1] = acc1;
     }
+    {
+      f32x4 acc0 = zero4(), acc1 = zero4();
+      const f32x4 a00 = lds_read4(a4p);
+      const f32x4 a01 = lds_read4(a4p + 16);
+      const f32x4 a10 = lds_read4(a4p + 16 * S_W4);
+      const f32x4 a11 = lds_read4(a4p + 16 * S_W4 + 16);
 #pragma unroll
-    for (int v = 0; v < 2; ++v) {
-      f32x4 acc = zero4();
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const f32x4 a = lds_read4(a4p + 16 * v * S_W4 + 16 * t);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma16(a[s], h3[t][s], acc);
+      for (int s = 0; s < 4; ++s) {
+        acc0 = mfma16(a00[s], h3[0][s], acc0);
+        acc1 = mfma16(a10[s], h3[0][s], acc1);
       }
-      y[v] = acc;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc0 = mfma16(a01[s], h3[1][s], acc0);
+        acc1 = mfma16(a11[s], h3[1][s], acc1);
+      }
+      y[0] = acc0;
+      y[1] = acc1;
     }
     float sq = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float d0 = y[0][r] - x0[r];
-      const float d1 = y[1][r] - x1[r];
-      sq += (xcol + r < d_in) ? d0 * d0 : 0.f;
-      sq += (xcol + 16 + r < d_in) ? d1 * d1 : 0.f;
+      const float d0 = (y[0][r] - x0[r]) * fm0[r];
+      const float d1 = (y[1][r] - x1[r]) * fm1[r];
+      sq += d0 * d0 + d1 * d1;
     }
     sq = (c < bcur) ? sq : 0.f;
     float nz = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) nz += (4 * g + r < latent) ? z[r] * z[r] : 0.f;
     nz = sum_lane_groups(nz);
-    norm_c = sqrtf(nz);
-    lacc += (double)sq / ((double)bcur * (double)d_in);
-    if (w == 0 && g == 0 && c < bcur) lacc += (double)A.lambda * (double)norm_c / (double)bcur;
+    norm_c = __builtin_amdgcn_sqrtf(nz);
+    const float inv_b = 1.0f / (float)bcur;
+    float contrib = sq * (inv_b * inv_d);
+    if (w == 0 && g == 0 && c < bcur) contrib += lam * norm_c * inv_b;
+    lacc += (double)contrib;
   };
 
   AdamStep K;
@@ -373,53 +420,73 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       forward(xa, xb, bcur, h1, z, zb, h3, y, norm_c, acc_tr);
       if (bi + 1 < nb) load_x(Xtr, row0 + B, min(B, n_tr - row0 - B), na, nbx);  // prefetch
 
+      // current W2a / W3a (all tiles, D layout) for the backward-data products;
+      // owners only rewrite the masters after barrier #2.
+      float q2[2][4], q3[2][4];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          q2[t][r] = d2p[r * S_W2 + 16 * t];
+          q3[t][r] = d3p[(16 * t + r) * S_W3];
+        }
+
       ++step;
       b1pow *= (double)A.beta1;
       b2pow *= (double)A.beta2;
       K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
       K.bc2s = (float)sqrt(1.0 - b2pow);
-      float prox_acc = 0.f;     // sum (p - anchor)^2 of owned params (pre-update)
-      float prox_acc_sh = 0.f;  // same for the replicated W2a/W3a (counted by wave 0)
+      K.inv_bc2s = 1.0f / K.bc2s;
+      float prox_acc = 0.f;  // sum (p - anchor)^2 of owned params (pre-update)
 
       // ---- dY (masked) and the transposes feeding dW4
-      const float scale = 2.0f / (float)(bcur * d_in);
+      const float scale = (c < bcur) ? 2.0f / (float)(bcur * d_in) : 0.f;
       f32x4 dy[2];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bool okb = c < bcur;
-        dy[0][r] = (okb && xcol + r < d_in) ? (y[0][r] - xa[r]) * scale : 0.f;
-        dy[1][r] = (okb && xcol + 16 + r < d_in) ? (y[1][r] - xb[r]) * scale : 0.f;
+        dy[0][r] = (y[0][r] - xa[r]) * (scale * fm0[r]);
+        dy[1][r] = (y[1][r] - xb[r]) * (scale * fm1[r]);
         sT0[tw + r * S_T] = dy[0][r];
         sT0[tw + (16 + r) * S_T] = dy[1][r];
         sT1[tw + r * S_T] = h3[0][r];
         sT1[tw + (16 + r) * S_T] = h3[1][r];
       }
       // ---- dH3 partial = W4a(own rows)^T dY(own rows)   (pre-update W4)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        f32x4 acc = zero4();
+      {
+        f32x4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
         for (int v = 0; v < 2; ++v)
 #pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma16(P.q4[v][t][s], dy[v][s], acc);
-        lds_write4(redw + t * 256, acc);
+          for (int s = 0; s < 4; ++s) {
+            acc0 = mfma16(P.q4[v][0][s], dy[v][s], acc0);
+            acc1 = mfma16(P.q4[v][1][s], dy[v][s], acc1);
+          }
+        lds_write4(redw, acc0);
+        lds_write4(redw + 256, acc1);
       }
       wave_sync();
       // ---- dW4 (own rows) + fused Adam
+      {
+        const f32x4 a0 = lds_read4(sT0 + tr);
+        const f32x4 a1 = lds_read4(sT0 + tr + 16 * S_T);
+        const f32x4 b0 = lds_read4(sT1 + tr);
+        const f32x4 b1 = lds_read4(sT1 + tr + 16 * S_T);
+        f32x4 g00 = zero4(), g01 = zero4(), g10 = zero4(), g11 = zero4();
 #pragma unroll
-      for (int v = 0; v < 2; ++v)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          f32x4 acc = zero4();
-          const f32x4 a = lds_read4(sT0 + tr + 16 * v * S_T);
-          const f32x4 b = lds_read4(sT1 + tr + 16 * t * S_T);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            adam_update<PROX>(P.q4[v][t][r], M.q4[v][t][r], V.q4[v][t][r], PROX ? AN.q4[v][t][r] : 0.f, acc[r], K,
-                              prox_acc);
+        for (int s = 0; s < 4; ++s) {
+          g00 = mfma16(a0[s], b0[s], g00);
+          g01 = mfma16(a0[s], b1[s], g01);
+          g10 = mfma16(a1[s], b0[s], g10);
+          g11 = mfma16(a1[s], b1[s], g11);
         }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          adam_update<PROX>(P.q4[0][0][r], M.q4[0][0][r], V.q4[0][0][r], PROX ? AN.q4[0][0][r] : 0.f, g00[r], K, prox_acc);
+          adam_update<PROX>(P.q4[0][1][r], M.q4[0][1][r], V.q4[0][1][r], PROX ? AN.q4[0][1][r] : 0.f, g01[r], K, prox_acc);
+          adam_update<PROX>(P.q4[1][0][r], M.q4[1][0][r], V.q4[1][0][r], PROX ? AN.q4[1][0][r] : 0.f, g10[r], K, prox_acc);
+          adam_update<PROX>(P.q4[1][1][r], M.q4[1][1][r], V.q4[1][1][r], PROX ? AN.q4[1][1][r] : 0.f, g11[r], K, prox_acc);
+        }
+      }
       // ---- stage X^T, H1^T, Z^T for the remaining weight gradients
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -438,7 +505,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         for (int ww = 1; ww < 4; ++ww) {
           const f32x4 o = lds_read4(sRedDH3 + (ww * 2 + t) * 256 + lane * 4);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s[r] = __fadd_rn(s[r], o[r]);
+          for (int r = 0; r < 4; ++r) s[r] = s[r] + o[r];
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -448,79 +515,77 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         }
         dh3[t] = s;
       }
-      wave_sync();
-      // ---- dZ = W3a^T dH3 (pre-update W3) ; dW3 = dH3^T Z (redundant) + Adam
+      // ---- dZ = W3a^T dH3 (pre-update W3, every wave)
       f32x4 dz = zero4();
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) dz = mfma16(P.q3[t][s], dh3[t][s], dz);
-      {
-        const f32x4 b = lds_read4(sZT + tr);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          f32x4 acc = zero4();
-          const f32x4 a = lds_read4(sT0 + tr + 16 * t * S_T);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            adam_update<PROX>(P.q3[t][r], M.q3[t][r], V.q3[t][r], PROX ? AN.q3[t][r] : 0.f, acc[r], K, prox_acc_sh);
-        }
-      }
+        for (int s = 0; s < 4; ++s) dz = mfma16(q3[t][s], dh3[t][s], dz);
       // shrink-loss gradient: lambda/B * z / ||z|| (0 where ||z|| == 0)
-      const float shr = (c < bcur && norm_c > 0.f) ? A.lambda / ((float)bcur * norm_c) : 0.f;
+      const float shr = (c < bcur && norm_c > 0.f) ? lam / ((float)bcur * norm_c) : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         dz[r] = (4 * g + r < latent) ? dz[r] + shr * z[r] : 0.f;
         sDZT[tw + r * S_T] = dz[r];
       }
       // ---- dH1 = W2a^T dZ (pre-update W2) -> dH1^T staged in sT1 (H3^T reads done)
+      {
+        f32x4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        f32x4 acc = zero4();
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma16(P.q2[t][s], dz[s], acc);
+        for (int s = 0; s < 4; ++s) {
+          acc0 = mfma16(q2[0][s], dz[s], acc0);
+          acc1 = mfma16(q2[1][s], dz[s], acc1);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int h = 16 * t + 4 * g + r;
-          sT1[tw + (16 * t + r) * S_T] = (h < hidden && h1[t][r] > 0.f) ? acc[r] : 0.f;
+          const int h0 = 4 * g + r, h1i = 16 + 4 * g + r;
+          sT1[tw + r * S_T] = (h0 < hidden && h1[0][r] > 0.f) ? acc0[r] : 0.f;
+          sT1[tw + (16 + r) * S_T] = (h1i < hidden && h1[1][r] > 0.f) ? acc1[r] : 0.f;
         }
       }
       wave_sync();
-      // ---- dW2 = dZ^T H1 (redundant) + Adam
+      // ---- owned small tile: w<2 -> dW3 tile (h-block w) = dH3^T Z ;
+      //                        w>=2 -> dW2 tile (h-block w-2) = dZ^T H1
       {
-        const f32x4 a = lds_read4(sDZT + tr);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          f32x4 acc = zero4();
-          const f32x4 b = lds_read4(sH1T + tr + 16 * t * S_T);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            adam_update<PROX>(P.q2[t][r], M.q2[t][r], V.q2[t][r], PROX ? AN.q2[t][r] : 0.f, acc[r], K, prox_acc_sh);
+        f32x4 a, b;
+        if (w < 2) {
+          a = lds_read4(sT0 + tr + 16 * w * S_T);
+          b = lds_read4(sZT + tr);
+        } else {
+          a = lds_read4(sDZT + tr);
+          b = lds_read4(sH1T + tr + 16 * (w - 2) * S_T);
         }
+        f32x4 acc = zero4();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) adam_update<PROX>(P.o[r], M.o[r], V.o[r], PROX ? AN.o[r] : 0.f, acc[r], K, prox_acc);
       }
       // ---- dW1 (own columns) = dH1^T X + fused Adam
+      {
+        const f32x4 a0 = lds_read4(sT1 + tr);
+        const f32x4 a1 = lds_read4(sT1 + tr + 16 * S_T);
+        const f32x4 b0 = lds_read4(sXT + tr);
+        const f32x4 b1 = lds_read4(sXT + tr + 16 * S_T);
+        f32x4 g00 = zero4(), g01 = zero4(), g10 = zero4(), g11 = zero4();
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const f32x4 a = lds_read4(sT1 + tr + 16 * t * S_T);
+        for (int s = 0; s < 4; ++s) {
+          g00 = mfma16(a0[s], b0[s], g00);
+          g01 = mfma16(a0[s], b1[s], g01);
+          g10 = mfma16(a1[s], b0[s], g10);
+          g11 = mfma16(a1[s], b1[s], g11);
+        }
 #pragma unroll
-        for (int v = 0; v < 2; ++v) {
-          f32x4 acc = zero4();
-          const f32x4 b = lds_read4(sXT + tr + 16 * v * S_T);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            adam_update<PROX>(P.q1[t][v][r], M.q1[t][v][r], V.q1[t][v][r], PROX ? AN.q1[t][v][r] : 0.f, acc[r], K,
-                              prox_acc);
+        for (int r = 0; r < 4; ++r) {
+          adam_update<PROX>(P.q1[0][0][r], M.q1[0][0][r], V.q1[0][0][r], PROX ? AN.q1[0][0][r] : 0.f, g00[r], K, prox_acc);
+          adam_update<PROX>(P.q1[0][1][r], M.q1[0][1][r], V.q1[0][1][r], PROX ? AN.q1[0][1][r] : 0.f, g01[r], K, prox_acc);
+          adam_update<PROX>(P.q1[1][0][r], M.q1[1][0][r], V.q1[1][0][r], PROX ? AN.q1[1][0][r] : 0.f, g10[r], K, prox_acc);
+          adam_update<PROX>(P.q1[1][1][r], M.q1[1][1][r], V.q1[1][1][r], PROX ? AN.q1[1][1][r] : 0.f, g11[r], K, prox_acc);
         }
       }
-      if (PROX) acc_tr += (double)A.mu * (double)(prox_acc + (w == 0 ? prox_acc_sh : 0.f));
-      wave_sync();
-      owned_to_lds(P, L);  // publish the updated parameters (wave-private regions)
+      if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
+      // publish the updated parameters (own W1 columns / W4 rows / small tile)
+      slab_to_lds(P, L);
       wave_sync();
       xa = na;
       xb = nbx;
@@ -539,22 +604,23 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
     }
     double prox_now = 0.0;
     if (PROX) {
-      float pr = 0.f, prs = 0.f;
+      float pr = 0.f;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int v = 0; v < 2; ++v) {
             const float d1 = P.q1[t][v][r] - AN.q1[t][v][r];
             const float d4 = P.q4[v][t][r] - AN.q4[v][t][r];
             pr += d1 * d1 + d4 * d4;
           }
-          const float d2 = P.q2[t][r] - AN.q2[t][r];
-          const float d3 = P.q3[t][r] - AN.q3[t][r];
-          prs += d2 * d2 + d3 * d3;
-        }
-      prox_now = (double)pr + (w == 0 ? (double)prs : 0.0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = P.o[r] - AN.o[r];
+        pr += d * d;
+      }
+      prox_now = (double)pr;
     }
     // ---- epoch-end reduction (fixed order over waves -> identical decision everywhere)
     {
@@ -584,7 +650,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       min_valid = valid_loss;
       best_ep = ep;
       worse = 0;
-      masters_to_global(Bg, sW1, sW4, sW23);  // save_model(): best-validation snapshot
+      masters_to_global(Bg, sW1, sW4, sW2, sW3);  // save_model(): best-validation snapshot
     } else {
       ++worse;
     }
@@ -593,15 +659,15 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   }
 
   // ---- write back: params (masters), then m and v through the same staging
-  masters_to_global(Pg, sW1, sW4, sW23);
+  masters_to_global(Pg, sW1, sW4, sW2, sW3);
   __syncthreads();
-  owned_to_lds(M, L);
+  slab_to_lds(M, L);
   __syncthreads();
-  masters_to_global(Mg, sW1, sW4, sW23);
+  masters_to_global(Mg, sW1, sW4, sW2, sW3);
   __syncthreads();
-  owned_to_lds(V, L);
+  slab_to_lds(V, L);
   __syncthreads();
-  masters_to_global(Vg, sW1, sW4, sW23);
+  masters_to_global(Vg, sW1, sW4, sW2, sW3);
   if (threadIdx.x == 0) {
     A.adam_step[cid] = step;
     A.epochs_run[kslot] = ep_run;

@@ -1,0 +1,165 @@
+// Small protocol kernels on gfx950 (all launch-latency sized; the point is to
+// keep every per-round reduction on the device so a round needs only a few
+// host synchronisations).
+//
+//  * score_reduce  : per-row SSE segments -> (vote score, mean MSE)
+//      vote score = mean over batches of 128 rows of the batch MSE
+//      (calculate_mse_score, src/Trainer/client_trainer.py:226-241);
+//      mean MSE   = sum SSE / (n * D) (fed_mse_avg / verifier,
+//      src/Trainer/client_trainer.py:118-124, src/Trainer/model_verifier.py:95-99)
+//  * broadcast_rows: dst[idx[i]] = src for the accepted receivers (adopt the
+//      aggregate + refresh the FedProx anchor, client_trainer.py:191-195)
+//  * standardize_ddof1 (LDS-staged): vote-data normalisation
+//      (client_trainer.py:220-223)
+#include "fedmx_common.h"
+
+namespace fedmx {
+
+struct SegDesc {
+  const float* sse;  // [n]
+  int32_t n;
+  int32_t batch;     // rows per vote batch (128); <= 0: single batch
+  double* out;       // [2]: vote score, mean MSE
+};
+static_assert(sizeof(SegDesc) == 24, "SegDesc layout is shared with Python");
+
+__global__ __launch_bounds__(256) void score_reduce_kernel(const SegDesc* __restrict__ descs, int d_in) {
+  const SegDesc d = descs[blockIdx.x];
+  __shared__ double s_tot[256];
+  __shared__ double s_vote[256];
+  const int tid = threadIdx.x;
+  const int bs = d.batch > 0 ? d.batch : (d.n > 0 ? d.n : 1);
+  const int nb = (d.n + bs - 1) / bs;
+  // thread t accumulates whole rows; batch means need per-batch sums: each thread
+  // owns batches t, t+256, ... and sums their rows (batches are contiguous).
+  double vote = 0.0, tot = 0.0;
+  for (int b = tid; b < nb; b += blockDim.x) {
+    const int r0 = b * bs;
+    const int r1 = min(d.n, r0 + bs);
+    double s = 0.0;
+    for (int r = r0; r < r1; ++r) s += (double)d.sse[r];
+    tot += s;
+    vote += s / ((double)(r1 - r0) * d_in);
+  }
+  s_tot[tid] = tot;
+  s_vote[tid] = vote;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      s_tot[tid] += s_tot[tid + o];
+      s_vote[tid] += s_vote[tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    d.out[0] = nb > 0 ? s_vote[0] / nb : __builtin_inf();
+    d.out[1] = d.n > 0 ? s_tot[0] / ((double)d.n * d_in) : __builtin_nan("");
+  }
+}
+
+__global__ __launch_bounds__(256) void broadcast_rows_kernel(float* __restrict__ dst0, float* __restrict__ dst1,
+                                                             const int32_t* __restrict__ idx, int n,
+                                                             const float* __restrict__ src, int P) {
+  const int i4 = blockIdx.x * blockDim.x + threadIdx.x;  // float4 index within a row
+  const int row = blockIdx.y;
+  if (row >= n || i4 * 4 >= P) return;
+  const f32x4 v = reinterpret_cast<const f32x4*>(src)[i4];
+  const size_t base = (size_t)idx[row] * P;
+  reinterpret_cast<f32x4*>(dst0 + base)[i4] = v;
+  if (dst1 != nullptr) reinterpret_cast<f32x4*>(dst1 + base)[i4] = v;
+}
+
+// (x - mean) / (std_unbiased + 1e-8) per real column.  Rows are staged in LDS
+// in chunks of up to 256 rows (128 KB); column sums in float64.
+constexpr int STD_CHUNK = 256;
+
+__global__ __launch_bounds__(256) void standardize_lds_kernel(const float* __restrict__ x, int n, int d_in,
+                                                              float* __restrict__ y) {
+  __shared__ __attribute__((aligned(16))) float tile[STD_CHUNK * DP];
+  __shared__ double s_part[2][DP];
+  __shared__ float s_mean[DP];
+  __shared__ float s_den[DP];
+  const int tid = threadIdx.x;
+  const int col = tid & (DP - 1);
+  const int half = tid >> 7;  // 0/1: row parity handled by this thread
+  double sum = 0.0;
+  for (int r0 = 0; r0 < n; r0 += STD_CHUNK) {
+    const int rows = min(STD_CHUNK, n - r0);
+    for (int i = tid; i < rows * DP / 4; i += 256)
+      reinterpret_cast<f32x4*>(tile)[i] = reinterpret_cast<const f32x4*>(x + (size_t)r0 * DP)[i];
+    __syncthreads();
+    for (int r = half; r < rows; r += 2) sum += (double)tile[r * DP + col];
+    __syncthreads();
+  }
+  s_part[half][col] = sum;
+  __syncthreads();
+  const double mean = (s_part[0][col] + s_part[1][col]) / n;
+  __syncthreads();
+  double q = 0.0;
+  const bool single = (n <= STD_CHUNK);
+  for (int r0 = 0; r0 < n; r0 += STD_CHUNK) {
+    const int rows = min(STD_CHUNK, n - r0);
+    if (!single) {
+      for (int i = tid; i < rows * DP / 4; i += 256)
+        reinterpret_cast<f32x4*>(tile)[i] = reinterpret_cast<const f32x4*>(x + (size_t)r0 * DP)[i];
+      __syncthreads();
+    }
+    for (int r = half; r < rows; r += 2) {
+      const double df = (double)tile[r * DP + col] - mean;
+      q += df * df;
+    }
+    __syncthreads();
+  }
+  s_part[half][col] = q;
+  __syncthreads();
+  if (half == 0) {
+    const double var = (s_part[0][col] + s_part[1][col]) / (n > 1 ? (n - 1) : 1);
+    s_mean[col] = (float)mean;
+    s_den[col] = (float)sqrt(var) + 1e-8f;
+  }
+  __syncthreads();
+  for (int r0 = 0; r0 < n; r0 += STD_CHUNK) {
+    const int rows = min(STD_CHUNK, n - r0);
+    if (!single) {
+      for (int i = tid; i < rows * DP / 4; i += 256)
+        reinterpret_cast<f32x4*>(tile)[i] = reinterpret_cast<const f32x4*>(x + (size_t)r0 * DP)[i];
+      __syncthreads();
+    }
+    for (int i = tid; i < rows * DP; i += 256) {
+      const int cc = i & (DP - 1);
+      y[(size_t)r0 * DP + i] = (cc < d_in) ? (tile[i] - s_mean[cc]) / s_den[cc] : 0.f;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace fedmx
+
+extern "C" {
+
+int fedmx_score_reduce(const void* descs, int n, int d_in, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(fedmx::score_reduce_kernel, dim3(n), dim3(256), 0, stream,
+                     reinterpret_cast<const fedmx::SegDesc*>(descs), d_in);
+  return (int)hipGetLastError();
+}
+
+int fedmx_broadcast_rows(float* dst0, float* dst1, const int32_t* idx, int n, const float* src, int P,
+                         hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (P % 4 != 0) return -1;
+  const int n4 = P / 4;
+  hipLaunchKernelGGL(fedmx::broadcast_rows_kernel, dim3((n4 + 255) / 256, n), dim3(256), 0, stream, dst0, dst1, idx,
+                     n, src, P);
+  return (int)hipGetLastError();
+}
+
+int fedmx_standardize_lds(const float* x, int n, int d_in, float* y, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(fedmx::standardize_lds_kernel, dim3(1), dim3(256), 0, stream, x, n, d_in, y);
+  return (int)hipGetLastError();
+}
+
+int fedmx_seg_desc_size() { return (int)sizeof(fedmx::SegDesc); }
+
+}  // extern "C"

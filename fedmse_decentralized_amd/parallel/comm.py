@@ -152,9 +152,11 @@ class TorchDistComm(Comm):
 
     def all_gather(self, t):
         x = self._to(t).contiguous()
-        out = torch.empty((self.world_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-        self.dist.all_gather_into_tensor(out, x)
-        return out.to(t.device)
+        flat = x.reshape(1, -1) if x.dim() == 0 else x
+        # concatenated-along-dim-0 form (supported by both gloo and RCCL)
+        out = torch.empty((self.world_size * flat.shape[0],) + tuple(flat.shape[1:]), dtype=x.dtype, device=x.device)
+        self.dist.all_gather_into_tensor(out, flat)
+        return out.view((self.world_size,) + tuple(x.shape)).to(t.device)
 
     def broadcast(self, t, src):
         x = self._to(t).clone()

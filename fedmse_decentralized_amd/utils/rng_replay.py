@@ -33,7 +33,9 @@ class TorchRngReplay:
         self.draws = 0
 
     def _run(self, fn):
-        with torch.random.fork_rng(devices=[]):
+        from ..models.reference import GLOBAL_RNG_LOCK
+
+        with GLOBAL_RNG_LOCK, torch.random.fork_rng(devices=[]):
             torch.set_rng_state(self.state)
             out = fn()
             self.state = torch.get_rng_state()

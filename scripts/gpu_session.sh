@@ -24,12 +24,21 @@ if [ "$MODE" = all ] || [ "$MODE" = test ]; then
   step pytest_gpu 420 python -m pytest tests -m gpu -x -q
   step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 fi
+if [ "$MODE" = all ] || [ "$MODE" = kernels ]; then
+  step bench_kernels 300 python scripts/bench_kernels.py
+fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 300 python bench.py --steps 20 --warmup 3 --out "$OUT/bench.json"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp && export TMPDIR=/tmp
   step rocprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 2
+  cd "$ROOT"
+fi
+if [ "$MODE" = pmc ]; then
+  cd /tmp && export TMPDIR=/tmp
+  rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
+  step pmc 300 rocprofv3 --kernel-trace --stats --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d "$OUT/pmc" -o pmc -- python3 "$ROOT/scripts/bench_kernels.py" --reps 3
   cd "$ROOT"
 fi
 echo "=== done"

@@ -1,0 +1,158 @@
+"""End-to-end federation on CPU (BASELINE config 1 plumbing): report schemas,
+checkpoint artefacts, resume, determinism across in-process ranks, fault
+injection."""
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from fedmse_decentralized_amd.config import ExperimentConfig
+from fedmse_decentralized_amd.federation import Federation
+from fedmse_decentralized_amd.parallel.comm import ThreadComm
+
+SMALL = dict(normal_rows=(90, 100), abnormal_rows=(120, 130), test_normal_rows=20)
+
+
+def _cfg(tmp_path, **kw):
+    base = dict(synthetic="nbaiot", network_size=4, num_rounds=3, epoch=2, batch_size=12,
+                output_root=str(tmp_path), backend="torch", device="cpu", log_level="WARNING",
+                model_types=["hybrid"], update_types=["mse_avg"])
+    base.update(kw)
+    return ExperimentConfig(**base)
+
+
+@pytest.fixture(autouse=True)
+def _small_synthetic(monkeypatch):
+    # shrink the synthetic clients so CPU tests stay fast
+    from fedmse_decentralized_amd.data import synthetic
+
+    orig = synthetic.SyntheticSpec.resolved
+
+    def resolved(self):
+        s = orig(self)
+        s.normal_rows, s.abnormal_rows, s.test_normal_rows = SMALL["normal_rows"], SMALL["abnormal_rows"], \
+            SMALL["test_normal_rows"]
+        return s
+    monkeypatch.setattr(synthetic.SyntheticSpec, "resolved", resolved)
+    from fedmse_decentralized_amd import federation
+    federation._PREP_CACHE.clear()
+
+
+def test_reports_and_artifacts(tmp_path):
+    cfg = _cfg(tmp_path, global_early_stop=False)
+    fed = Federation(cfg, "hybrid", "mse_avg", 0).setup()
+    best = fed.run_all()
+    assert 0.5 < best <= 1.0
+    res = os.path.join(cfg.checkpoint_dir, "Run_0", "AUC", "FL-IoT_0.5_hybrid_mse_avg_results.json")
+    lines = [json.loads(l) for l in open(res)]
+    assert [l["round"] for l in lines] == [1, 2, 3]
+    for l in lines:
+        assert set(l) == {"round", "client_metrics", "update_type", "model_type", "global_loss"}
+        assert len(l["client_metrics"]) == 4 and l["global_loss"] == min(l["client_metrics"])
+    ver = [json.loads(l) for l in open(os.path.join(cfg.checkpoint_dir, "Run_0", "verification_results.json"))]
+    for v in ver:
+        assert len(v["verification_results"]) == 3     # everyone but the aggregator
+        for r in v["verification_results"]:
+            assert set(r) == {"client_id", "rejected_updates", "is_verified"}
+    # model.cpt of every client trained at least once, loadable with weights_only
+    cpts = []
+    for root, _, files in os.walk(os.path.join(str(tmp_path), "Checkpoint", "4")):
+        if "model.cpt" in files:
+            cpts.append(os.path.join(root, "model.cpt"))
+    assert cpts
+    sd = torch.load(cpts[0], weights_only=True)
+    assert list(sd.keys())[0] == "encoder.encoder_network.0.weight" and sd[list(sd.keys())[0]].shape == (27, 115)
+
+
+def test_model_cpt_bytes_match_reference_writer(tmp_path):
+    from fedmse_decentralized_amd.io.checkpoint import save_model_cpt
+    from fedmse_decentralized_amd.models.layout import canonical_to_padded, state_dict_to_canonical
+    from fedmse_decentralized_amd.models.reference import ReferenceSAE
+
+    m = ReferenceSAE()
+    ref = tmp_path / "ref.cpt"
+    torch.save(m.state_dict(), ref, _use_new_zipfile_serialization=False)
+    ours = save_model_cpt(str(tmp_path / "ours"), canonical_to_padded(state_dict_to_canonical(m.state_dict())))
+    # the legacy format keys (and orders) storages by memory address, so two
+    # saves of the same state differ only there: compare size, pickle header
+    # and content
+    ra, rb_ = open(ours, "rb").read(), open(ref, "rb").read()
+    assert len(ra) == len(rb_) and ra[:200] == rb_[:200]
+    a = torch.load(ours, weights_only=True)
+    b = torch.load(ref, weights_only=True)
+    assert list(a) == list(b) and all(torch.equal(a[k], b[k]) for k in a)
+
+
+def test_resume_reproduces_trajectory(tmp_path):
+    cfg = _cfg(tmp_path, global_early_stop=False, num_rounds=4, save_checkpoints=False)
+    a = Federation(cfg, "hybrid", "avg", 0).setup()
+    for _ in range(2):
+        a.run_round()
+    snap = a.save_snapshot(str(tmp_path / "snap.pt"))
+    ra = [a.run_round().metrics for _ in range(2)]
+    cfg2 = _cfg(tmp_path, global_early_stop=False, num_rounds=4, save_checkpoints=False, resume=snap)
+    b = Federation(cfg2, "hybrid", "avg", 0).setup()
+    assert b.round_idx == 2
+    rb = [b.run_round().metrics for _ in range(2)]
+    for x, y in zip(ra, rb):
+        np.testing.assert_array_equal(x, y)
+
+
+def _run_threads(world, cfg, rounds):
+    comms = ThreadComm.group(world)
+    out = [None] * world
+    errs = []
+
+    def worker(r):
+        try:
+            f = Federation(cfg, "hybrid", "mse_avg", 0, comm=comms[r], device=torch.device("cpu")).setup()
+            out[r] = [f.run_round() for _ in range(rounds)] + [f.engine.store.params.clone(), f.local]
+        except Exception as e:  # pragma: no cover
+            import traceback
+            errs.append(traceback.format_exc())
+            for c in comms:
+                c.g.barrier.abort()
+
+    ts = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs[0]
+    return out
+
+
+@pytest.mark.parametrize("compat", ["reference", "fixed"])
+def test_sharded_federation_matches_single_rank(tmp_path, compat):
+    cfg = _cfg(tmp_path, global_early_stop=False, save_checkpoints=False, compat=compat, network_size=5)
+    single = _run_threads(1, cfg, 3)[0]
+    for world in (2, 3):
+        outs = _run_threads(world, cfg, 3)
+        for r in range(3):
+            for o in outs:
+                assert o[r].aggregator == single[r].aggregator
+                assert o[r].selected == single[r].selected
+                np.testing.assert_array_equal(o[r].metrics, single[r].metrics)
+        # every rank's shard equals the same clients' params of the single-rank run
+        for o in outs:
+            params, local = o[3], o[4]
+            assert torch.equal(params, single[3][local[0]:local[-1] + 1])
+
+
+def test_malicious_client_gets_rejected(tmp_path):
+    cfg = _cfg(tmp_path, global_early_stop=False, save_checkpoints=False, num_participants=1.0, network_size=3,
+               malicious_clients=[0, 1, 2], malicious_scale=50.0, num_rounds=3, update_types=["avg"])
+    fed = Federation(cfg, "hybrid", "avg", 0).setup()
+    results = [fed.run_round() for _ in range(3)]
+    later = [v for r in results[1:] for v in r.verification]
+    assert any(not v["is_verified"] for v in later)
+
+
+def test_global_early_stop_compat(tmp_path):
+    cfg = _cfg(tmp_path, num_rounds=10, save_checkpoints=False)
+    fed = Federation(cfg, "hybrid", "avg", 0).setup()
+    fed.run_all()
+    assert fed.round_idx < 10   # AUC compared like a loss stops early (Q8)
