@@ -58,6 +58,7 @@ def main(argv=None):
     p.add_argument("--no-artifacts", action="store_true", help="skip model.cpt/tracking/JSONL writes")
     p.add_argument("--trace", default=None, help="per-phase JSONL trace (adds device syncs)")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
+    p.add_argument("--profile", default=None, help="cProfile the timed rounds (rank 0) into this file")
     args = p.parse_args(argv)
 
     from fedmse_decentralized_amd.config import ExperimentConfig
@@ -93,11 +94,26 @@ def main(argv=None):
     comm.barrier()
     if device == "cuda":
         torch.cuda.synchronize()
+    prof = None
+    if args.profile and comm.is_root:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     last = None
     for _ in range(args.steps):
         last = one_round()
     fed.writer.flush()   # artefacts of the timed rounds are on disk before the clock stops
+    if prof is not None:
+        prof.disable()
+        import io
+        import pstats
+
+        s = io.StringIO()
+        pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(40)
+        with open(args.profile, "w") as f:
+            f.write(s.getvalue())
     comm.barrier()
     if device == "cuda":
         torch.cuda.synchronize()

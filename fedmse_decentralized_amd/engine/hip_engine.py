@@ -38,7 +38,7 @@ class HipEngine(Engine):
             raise RuntimeError("HipEngine requires a GPU device")
         _hip.lib()  # load (and fail loudly) up front
         self._seg = segment_ids_padded(dims).to(self.device)
-        self._stage = _hip.HostStage(self.device)
+        self._rt = _hip.runtime(self.device)
         self._eval_plans: Dict[str, dict] = {}
         self._vs = None
 
@@ -48,24 +48,21 @@ class HipEngine(Engine):
         self.store._train_bufs = None
 
     # -- transfers -----------------------------------------------------------------
-    def fetch(self, tensors: Sequence[torch.Tensor]) -> List[np.ndarray]:
-        out: List[Optional[np.ndarray]] = [None] * len(tensors)
-        dev_idx = []
-        for i, t in enumerate(tensors):
-            if t.device.type == "cpu":
-                out[i] = t.detach().numpy()
+    def fetch(self, items: Sequence) -> List[np.ndarray]:
+        """One stream synchronisation, then host copies.  Items are host views
+        written by kernels (mapped pinned memory) or device tensors."""
+        self._rt.sync()
+        out = []
+        for t in items:
+            if isinstance(t, (np.ndarray, _VoteView, _ColView)):
+                out.append(t.copy())
             else:
-                dev_idx.append(i)
-                self._stage.add(t)
-        if dev_idx:
-            res = self._stage.fetch()
-            for i, r in zip(dev_idx, res):
-                out[i] = r
+                out.append(t.detach().cpu().numpy())
         return out
 
     # -- training ------------------------------------------------------------------
     def train_launch(self, local_ids: Sequence[int], hp: TrainHParams) -> TrainHandle:
-        trk, er, be = _hip.train(self.store, list(local_ids), hp, self.dims, getattr(self.store, "_train_bufs", None))
+        trk, er, be = _hip.train(self.store, list(local_ids), hp, self.dims)
         return TrainHandle(list(local_ids), [trk, er, be])
 
     def train_collect(self, handle: TrainHandle, host: Optional[List[np.ndarray]] = None) -> TrainResult:
@@ -111,9 +108,10 @@ class HipEngine(Engine):
 
     # -- round operations ------------------------------------------------------------
     def vote_scores(self, local_rows, vote_data, dev_set, vote_bs):
+        """Host view [k, 2] (vote score, dev MSE) written by the kernels."""
         k = len(local_rows)
         if k == 0:
-            return torch.zeros(0, 2, dtype=torch.float64, device=self.device)
+            return np.zeros((0, 2), dtype=np.float64)
         if self._vs is None or self._vs.shape[0] < vote_data.shape[0]:
             self._vs = torch.empty(max(vote_data.shape[0], 256), 128, dtype=torch.float32, device=self.device)
         vs = self._vs[:vote_data.shape[0]]
@@ -123,20 +121,19 @@ class HipEngine(Engine):
             items += [(c, dev_set) for c in local_rows]
         sse, _ = _hip.forward_rows(self.store.params, items, self.dims, True, False)
         red = _hip.score_reduce(sse, [vote_bs] * k + [0] * (len(sse) - k), self.dims.d_in)
-        out = torch.full((k, 2), float("nan"), dtype=torch.float64, device=self.device)
-        out[:, 0] = red[:k, 0]
-        if dev_set is not None:
-            out[:, 1] = red[k:, 1]
-        return out
+        return _VoteView(red, k, dev_set is not None)
 
     def verify_stats(self, agg, datasets, hist):
+        """(host view of MSEs, host view of drifts) written by the kernels."""
         if datasets:
             sse, _ = _hip.forward_rows(agg.unsqueeze(0), [(0, x) for x in datasets], self.dims, True, False)
-            mse = _hip.score_reduce(sse, [0] * len(sse), self.dims.d_in)[:, 1]
+            mse = _ColView(_hip.score_reduce(sse, [0] * len(sse), self.dims.d_in), 1)
         else:
-            mse = torch.zeros(0, dtype=torch.float64, device=self.device)
-        drift = self.param_drift(hist, agg) if hist is not None and hist.shape[0] else \
-            torch.zeros(0, dtype=torch.float32, device=self.device)
+            mse = np.zeros(0, dtype=np.float64)
+        if hist is not None and hist.shape[0]:
+            drift = _hip.param_drift(hist, agg, self._seg, to_host=True)
+        else:
+            drift = np.zeros(0, dtype=np.float32)
         return mse, drift
 
     def adopt(self, local_rows, agg, anchor=True):
@@ -150,7 +147,8 @@ class HipEngine(Engine):
         st = self.store
         C = st.num_clients
         labels = [st.label_view(c) for c in range(C)]
-        aucs = torch.empty(C, dtype=torch.float64, device=self.device)
+        aucs_buf = _hip._hiprt.MappedBuffer(max(8 * C, 64))   # AUCs written straight to host memory
+        aucs = aucs_buf.view(0, np.float64, C)
         if model_type == "hybrid":
             items = []
             for c in range(C):
@@ -161,25 +159,26 @@ class HipEngine(Engine):
                                      dtype=torch.float64, device=self.device)
             cdesc, scores = _hip.cen_desc(lat[0::2], lat[1::2], scores_all, self.dims.latent)
             cdesc_dev = torch.from_numpy(cdesc.view(np.uint8).copy()).to(self.device)
-            adesc = _hip.auc_desc(scores, labels, aucs, 1.0)
+            adesc = _hip.auc_desc(scores, labels, aucs_buf.dev_ptr, 1.0)
             p = dict(fwd=fwd, cen=cdesc_dev, ncen=C, scores=scores, test_lat=lat[1::2])
         elif model_type == "autoencoder":
             fwd = _hip.FwdPlan(st.params, [(c, st.rows("test", c)) for c in range(C)], self.dims,
                                want_sse=True, want_latent=False)
             scores = fwd.sse_views()
-            adesc = _hip.auc_desc(scores, labels, aucs, 1.0 / self.dims.d_in)
+            adesc = _hip.auc_desc(scores, labels, aucs_buf.dev_ptr, 1.0 / self.dims.d_in)
             p = dict(fwd=fwd, cen=None, ncen=0, scores=scores, test_lat=None)
         else:
             raise ValueError(f"unknown model_type {model_type!r}")
         p["auc"] = torch.from_numpy(adesc.view(np.uint8).copy()).to(self.device)
         p["aucs"] = aucs
+        p["aucs_buf"] = aucs_buf
         p["labels"] = labels
         self._eval_plans[model_type] = p
         return p
 
-    def evaluate_launch(self, model_type: str) -> torch.Tensor:
+    def evaluate_launch(self, model_type: str) -> np.ndarray:
         """Enqueue the full AUC evaluation of every hosted client; returns the
-        device tensor of AUCs (float64 [C])."""
+        host view of the AUCs (float64 [C], valid after the next sync)."""
         p = self._plan(model_type)
         p["fwd"].run()
         if p["cen"] is not None:
@@ -201,3 +200,26 @@ class HipEngine(Engine):
             latents = [(l.detach().cpu().numpy().astype(np.float32), st.labels(c).astype(np.float32))
                        for c, l in enumerate(p["test_lat"])]
         return EvalResult(np.asarray(vals, dtype=np.float64), {}, latents)
+
+
+class _VoteView:
+    """Lazy [k, 2] view over score_reduce output: (vote score of the vote
+    segments, dev MSE of the dev segments)."""
+
+    def __init__(self, red: np.ndarray, k: int, has_dev: bool):
+        self.red, self.k, self.has_dev = red, k, has_dev
+
+    def copy(self):
+        out = np.full((self.k, 2), np.nan)
+        out[:, 0] = self.red[:self.k, 0]
+        if self.has_dev:
+            out[:, 1] = self.red[self.k:2 * self.k, 1]
+        return out
+
+
+class _ColView:
+    def __init__(self, a: np.ndarray, col: int):
+        self.a, self.col = a, col
+
+    def copy(self):
+        return self.a[:, self.col].copy()

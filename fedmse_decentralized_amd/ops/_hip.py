@@ -1,15 +1,15 @@
 """ctypes bindings of ``libfedmx_hip.so`` (hand-written gfx950 kernels).
 
 The library has a plain C ABI (no torch headers); device memory is owned by
-torch tensors and passed as raw pointers together with the current HIP
-stream, so the kernels interleave correctly with torch work on that stream.
+torch tensors and passed as raw pointers together with the stream.
 
-Work lists (forward row blocks, CEN / AUC / score jobs) are small descriptor
-arrays.  They are built with vectorised numpy and either
-* cached on the device for static work (every round evaluates the same
-  clients on the same buffers: ``Plan`` objects), or
-* staged through a pinned host ring and copied asynchronously on the stream
-  (``Uploader``) for per-round work — no pageable copies, no host syncs.
+Host<->device protocol traffic avoids the torch copy machinery entirely
+(``_hiprt``): descriptor arrays for per-round work are written into a mapped
+pinned ring that kernels read directly, static work lists (the per-round
+evaluation of every hosted client) are cached in device memory, and small
+results (scores, drifts, AUCs, training tracking) are written by the kernels
+straight into mapped pinned memory, read after one stream synchronisation
+per protocol phase.
 
 Loading fails loudly: on a GPU box the HIP engine must run these kernels,
 never a silent PyTorch fallback.
@@ -18,12 +18,12 @@ from __future__ import annotations
 
 import ctypes
 import threading
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 
-from . import build
+from . import _hiprt, build
 
 _lock = threading.Lock()
 _lib = None
@@ -98,104 +98,37 @@ def lib():
     return _lib
 
 
-def _stream(device: torch.device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
-
-
 def _check(rc: int, what: str):
     if rc != 0:
         raise RuntimeError(f"{what} failed with HIP error code {rc}")
 
 
-# ---------------------------------------------------------------------------
-class Uploader:
-    """Pinned host ring -> device ring, asynchronous on the current stream.
+class Runtime:
+    """Per-device launch context: the stream plus the mapped descriptor / result rings."""
 
-    A slot is reused only after the event recorded behind its copy has
-    completed, so the host never overwrites bytes a pending copy still reads;
-    device slots are consumed by kernels enqueued on the same stream before the
-    slot's next copy, so stream order protects them.
-    """
-
-    def __init__(self, device: torch.device, slot_bytes: int = 1 << 16, nslots: int = 64):
+    def __init__(self, device: torch.device):
         self.device = device
-        self.slot = slot_bytes
-        self.n = nslots
-        self.host = torch.empty(nslots * slot_bytes, dtype=torch.uint8).pin_memory()
-        self.host_np = self.host.numpy()
-        self.dev = torch.empty(nslots * slot_bytes, dtype=torch.uint8, device=device)
-        self.events: List[Optional[torch.cuda.Event]] = [None] * nslots
-        self.i = 0
+        self.stream = torch.cuda.current_stream(device).cuda_stream
+        self.desc = _hiprt.DescRing(4 << 20, self.stream)
+        self.out = _hiprt.OutRing(4 << 20, self.stream)
 
-    def upload(self, *arrays: np.ndarray) -> List[int]:
-        """Copy one or more arrays in one transfer; returns their device addresses."""
-        blobs = [np.ascontiguousarray(a).view(np.uint8).reshape(-1) for a in arrays]
-        offs, tot = [], 0
-        for b in blobs:
-            offs.append(tot)
-            tot += (b.nbytes + 15) & ~15
-        if tot > self.slot:
-            t = torch.from_numpy(np.concatenate([np.pad(b, (0, ((b.nbytes + 15) & ~15) - b.nbytes)) for b in blobs]))
-            d = t.to(self.device)
-            self._keep = d   # large, rare: plain copy (kept alive until next call)
-            return [d.data_ptr() + o for o in offs]
-        s = self.i
-        self.i = (self.i + 1) % self.n
-        ev = self.events[s]
-        if ev is not None:
-            ev.synchronize()
-        base = s * self.slot
-        for b, o in zip(blobs, offs):
-            self.host_np[base + o: base + o + b.nbytes] = b
-        self.dev[base:base + tot].copy_(self.host[base:base + tot], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        self.events[s] = ev
-        ptr = self.dev.data_ptr() + base
-        return [ptr + o for o in offs]
+    def sync(self):
+        _hiprt.stream_sync(self.stream)
 
 
-_uploaders = {}
+_runtimes: Dict[Tuple[str, int], Runtime] = {}
 
 
-def uploader(device: torch.device) -> Uploader:
-    key = (device.type, device.index)
-    u = _uploaders.get(key)
-    if u is None:
-        u = _uploaders[key] = Uploader(device)
-    return u
+def runtime(device: torch.device) -> Runtime:
+    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    r = _runtimes.get(key)
+    if r is None:
+        r = _runtimes[key] = Runtime(torch.device("cuda", key[1]))
+    return r
 
 
-class HostStage:
-    """Pinned staging for device->host readbacks: enqueue several async copies,
-    then one event wait (one host sync per protocol phase)."""
-
-    def __init__(self, device: torch.device, nbytes: int = 1 << 20):
-        self.device = device
-        self.buf = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
-        self.off = 0
-        self.items = []
-
-    def add(self, t: torch.Tensor):
-        t = t.contiguous()
-        nb = t.numel() * t.element_size()
-        off = (self.off + 15) & ~15
-        if off + nb > self.buf.numel():
-            raise RuntimeError("HostStage overflow")
-        dst = self.buf[off:off + nb].view(t.dtype).view(t.shape)
-        dst.copy_(t, non_blocking=True)
-        self.off = off + nb
-        self.items.append(dst)
-        return len(self.items) - 1
-
-    def fetch(self) -> List[np.ndarray]:
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        ev.synchronize()
-        out = [x.numpy().copy() for x in self.items]
-        self.items = []
-        self.off = 0
-        return out
+def _stream(device: torch.device) -> int:
+    return runtime(device).stream
 
 
 # ---------------------------------------------------------------------------
@@ -220,14 +153,19 @@ def build_fwd_desc(param_ptrs: np.ndarray, x_ptrs: np.ndarray, nrows: np.ndarray
     return desc
 
 
-def forward_rows(params: torch.Tensor, items, dims, want_sse=True, want_latent=False):
-    """items: sequence of (param_row, x[n, DP]).  Returns (sse list, latent list)."""
-    dev = params.device
-    sizes = np.array([int(x.shape[0]) for _, x in items], dtype=np.int64)
-    tot = int(sizes.sum())
+def _check_rows(items, dev):
     for _, x in items:
         if x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != 128 or not x.is_contiguous() or x.device != dev:
             raise ValueError("forward_rows expects contiguous float32 [n, 128] inputs on the params device")
+
+
+def forward_rows(params: torch.Tensor, items, dims, want_sse=True, want_latent=False):
+    """items: sequence of (param_row, x[n, DP]).  Returns (sse list, latent list) on device."""
+    dev = params.device
+    _check_rows(items, dev)
+    rt = runtime(dev)
+    sizes = np.array([int(x.shape[0]) for _, x in items], dtype=np.int64)
+    tot = int(sizes.sum())
     sse_all = torch.empty(tot, dtype=torch.float32, device=dev) if want_sse else None
     lat_all = torch.empty(tot, dims.latent, dtype=torch.float32, device=dev) if want_latent else None
     offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
@@ -238,14 +176,10 @@ def forward_rows(params: torch.Tensor, items, dims, want_sse=True, want_latent=F
     lptr = (lat_all.data_ptr() + 4 * dims.latent * offs) if want_latent else np.zeros(len(items), np.int64)
     desc = build_fwd_desc(pptr, xptr, sizes, sptr, lptr, dims)
     if len(desc):
-        (dptr,) = uploader(dev).upload(desc)
-        _check(lib().fedmx_forward_rows(dptr, len(desc), _stream(dev)), "fedmx_forward_rows")
-    sse_l, lat_l = [], []
-    for o, n in zip(offs, sizes):
-        if want_sse:
-            sse_l.append(sse_all[o:o + n])
-        if want_latent:
-            lat_l.append(lat_all[o:o + n])
+        (dptr,) = rt.desc.put(desc)
+        _check(lib().fedmx_forward_rows(dptr, len(desc), rt.stream), "fedmx_forward_rows")
+    sse_l = [sse_all[o:o + n] for o, n in zip(offs, sizes)] if want_sse else []
+    lat_l = [lat_all[o:o + n] for o, n in zip(offs, sizes)] if want_latent else []
     return sse_l, lat_l
 
 
@@ -253,8 +187,9 @@ class FwdPlan:
     """A cached forward launch over fixed (param row, buffer) items."""
 
     def __init__(self, params: torch.Tensor, items, dims, want_sse: bool, want_latent: bool):
-        self.params = params
         dev = params.device
+        _check_rows(items, dev)
+        self.params = params
         self.device = dev
         self.sizes = np.array([int(x.shape[0]) for _, x in items], dtype=np.int64)
         tot = int(self.sizes.sum())
@@ -302,14 +237,15 @@ def cen_desc(train_lat, test_lat, out: torch.Tensor, latent: int) -> Tuple[np.nd
 
 def cen_scores(train_lat: Sequence[torch.Tensor], test_lat: Sequence[torch.Tensor], latent: int):
     dev = train_lat[0].device
+    rt = runtime(dev)
     out_all = torch.empty(sum(int(t.shape[0]) for t in test_lat), dtype=torch.float64, device=dev)
     desc, views = cen_desc(train_lat, test_lat, out_all, latent)
-    (dptr,) = uploader(dev).upload(desc)
-    _check(lib().fedmx_cen_score(dptr, len(desc), _stream(dev)), "fedmx_cen_score")
+    (dptr,) = rt.desc.put(desc)
+    _check(lib().fedmx_cen_score(dptr, len(desc), rt.stream), "fedmx_cen_score")
     return views
 
 
-def auc_desc(scores, labels, out: torch.Tensor, f32_scale: float = 1.0) -> np.ndarray:
+def auc_desc(scores, labels, out_ptr: int, f32_scale: float = 1.0) -> np.ndarray:
     n = len(scores)
     desc = np.zeros(n, dtype=AUC_DTYPE)
     for i, (s, l) in enumerate(zip(scores, labels)):
@@ -317,22 +253,24 @@ def auc_desc(scores, labels, out: torch.Tensor, f32_scale: float = 1.0) -> np.nd
             raise ValueError("labels must be int32")
         desc[i]["score"] = s.data_ptr()
         desc[i]["label"] = l.data_ptr()
-        desc[i]["out"] = out.data_ptr() + 8 * i
+        desc[i]["out"] = out_ptr + 8 * i
         desc[i]["n"] = s.shape[0]
         desc[i]["score_is_f64"] = 1 if s.dtype == torch.float64 else 0
         desc[i]["score_scale"] = f32_scale
     return desc
 
 
-def auc(scores: Sequence[torch.Tensor], labels: Sequence[torch.Tensor], f32_scale: float = 1.0) -> torch.Tensor:
-    """Exact tie-aware ROC-AUC per (scores, labels) pair; float64 [n] on device.
+def auc(scores: Sequence[torch.Tensor], labels: Sequence[torch.Tensor], f32_scale: float = 1.0) -> np.ndarray:
+    """Exact tie-aware ROC-AUC per (scores, labels) pair.  Returns a float64
+    host view written by the kernel (valid after ``runtime(dev).sync()``);
     -1 marks classes too large for the LDS sort (caller uses the host path)."""
     dev = scores[0].device
-    out = torch.empty(len(scores), dtype=torch.float64, device=dev)
-    desc = auc_desc(scores, labels, out, f32_scale)
-    (dptr,) = uploader(dev).upload(desc)
-    _check(lib().fedmx_auc(dptr, len(desc), _stream(dev)), "fedmx_auc")
-    return out
+    rt = runtime(dev)
+    optr, view = rt.out.take(np.float64, len(scores))
+    desc = auc_desc(scores, labels, optr, f32_scale)
+    (dptr,) = rt.desc.put(desc)
+    _check(lib().fedmx_auc(dptr, len(desc), rt.stream), "fedmx_auc")
+    return view
 
 
 def launch_cen(desc_dev: torch.Tensor, n: int, device):
@@ -343,47 +281,56 @@ def launch_auc(desc_dev: torch.Tensor, n: int, device):
     _check(lib().fedmx_auc(desc_dev.data_ptr(), n, _stream(device)), "fedmx_auc")
 
 
-def score_reduce(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in: int) -> torch.Tensor:
-    """[len, 2] float64: (mean over batches of batch-MSE, overall MSE) per SSE segment."""
+def score_reduce(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in: int) -> np.ndarray:
+    """Host view [len, 2] float64: (mean over batches of batch-MSE, overall MSE)
+    per SSE segment; valid after the next stream sync."""
     dev = sse_list[0].device
-    out = torch.empty(len(sse_list), 2, dtype=torch.float64, device=dev)
+    rt = runtime(dev)
+    optr, view = rt.out.take(np.float64, 2 * len(sse_list))
     desc = np.zeros(len(sse_list), dtype=SEG_DTYPE)
     desc["sse"] = [s.data_ptr() for s in sse_list]
     desc["n"] = [int(s.shape[0]) for s in sse_list]
     desc["batch"] = list(batch)
-    desc["out"] = out.data_ptr() + 16 * np.arange(len(sse_list), dtype=np.int64)
-    (dptr,) = uploader(dev).upload(desc)
-    _check(lib().fedmx_score_reduce(dptr, len(desc), d_in, _stream(dev)), "fedmx_score_reduce")
-    return out
+    desc["out"] = optr + 16 * np.arange(len(sse_list), dtype=np.int64)
+    (dptr,) = rt.desc.put(desc)
+    _check(lib().fedmx_score_reduce(dptr, len(desc), d_in, rt.stream), "fedmx_score_reduce")
+    return view.reshape(len(sse_list), 2)
 
 
 def broadcast_rows(dst0: torch.Tensor, dst1: Optional[torch.Tensor], rows: Sequence[int], src: torch.Tensor):
-    dev = dst0.device
     if not len(rows):
         return
-    (iptr,) = uploader(dev).upload(np.asarray(rows, dtype=np.int32))
+    rt = runtime(dst0.device)
+    (iptr,) = rt.desc.put(np.asarray(rows, dtype=np.int32))
     _check(lib().fedmx_broadcast_rows(dst0.data_ptr(), 0 if dst1 is None else dst1.data_ptr(), iptr, len(rows),
-                                      src.data_ptr(), dst0.shape[1], _stream(dev)), "fedmx_broadcast_rows")
+                                      src.data_ptr(), dst0.shape[1], rt.stream), "fedmx_broadcast_rows")
 
 
 def weighted_sum(stack: torch.Tensor, weights: Sequence[float], out: Optional[torch.Tensor] = None) -> torch.Tensor:
     dev = stack.device
+    rt = runtime(dev)
     K, P = stack.shape
-    (wptr,) = uploader(dev).upload(np.asarray(weights, dtype=np.float32))
+    (wptr,) = rt.desc.put(np.asarray(weights, dtype=np.float32))
     if out is None:
         out = torch.empty(P, dtype=torch.float32, device=dev)
     st = stack.contiguous()
-    _check(lib().fedmx_weighted_sum(st.data_ptr(), wptr, K, P, out.data_ptr(), _stream(dev)), "fedmx_weighted_sum")
+    _check(lib().fedmx_weighted_sum(st.data_ptr(), wptr, K, P, out.data_ptr(), rt.stream), "fedmx_weighted_sum")
     return out
 
 
-def param_drift(hist: torch.Tensor, new: torch.Tensor, seg: torch.Tensor) -> torch.Tensor:
+def param_drift(hist: torch.Tensor, new: torch.Tensor, seg: torch.Tensor, to_host: bool = False):
+    """Per-row drift; a device tensor, or (``to_host``) a host view valid after the next sync."""
     dev = hist.device
+    rt = runtime(dev)
     M = hist.shape[0]
-    out = torch.empty(M, dtype=torch.float32, device=dev)
     h = hist.contiguous()
     nw = new.contiguous()
-    _check(lib().fedmx_param_drift(h.data_ptr(), M, nw.data_ptr(), seg.data_ptr(), out.data_ptr(), _stream(dev)),
+    if to_host:
+        optr, out = rt.out.take(np.float32, M)
+    else:
+        out = torch.empty(M, dtype=torch.float32, device=dev)
+        optr = out.data_ptr()
+    _check(lib().fedmx_param_drift(h.data_ptr(), M, nw.data_ptr(), seg.data_ptr(), optr, rt.stream),
            "fedmx_param_drift")
     return out
 
@@ -397,30 +344,29 @@ def standardize_ddof1(x: torch.Tensor, d_in: int, out: Optional[torch.Tensor] = 
 
 
 class TrainBuffers:
-    """Persistent per-store device buffers for the training launch outputs."""
+    """Persistent per-store device buffers for the training launch."""
 
-    def __init__(self, store, max_epochs: int):
+    def __init__(self, store):
         dev = store.params.device
-        C = store.num_clients
-        self.max_epochs = max_epochs
-        self.tracking = torch.empty(C, max_epochs, 2, dtype=torch.float64, device=dev)
-        self.epochs_run = torch.zeros(C, dtype=torch.int32, device=dev)
-        self.best_epoch = torch.zeros(C, dtype=torch.int32, device=dev)
         self.train_off = torch.from_numpy(store.train_off).to(dev)
         self.valid_off = torch.from_numpy(store.valid_off).to(dev)
 
 
-def train(store, local_ids: Sequence[int], hp, dims, bufs: Optional[TrainBuffers] = None):
+def train(store, local_ids: Sequence[int], hp, dims):
     """Launch the fused training kernel for store rows ``local_ids`` (async).
-    Returns (tracking[k, E, 2], epochs_run[k], best_epoch[k]) device views."""
+    Returns host views (tracking[k, E, 2], epochs_run[k], best_epoch[k])
+    written by the kernel, valid after the next stream sync."""
     dev = store.params.device
+    rt = runtime(dev)
     k = len(local_ids)
+    bufs = getattr(store, "_train_bufs", None)
     if bufs is None:
-        bufs = getattr(store, "_train_bufs", None)
-    if bufs is None or bufs.max_epochs < hp.epochs or bufs.tracking.shape[0] < k:
-        bufs = TrainBuffers(store, max(hp.epochs, 1))
-        store._train_bufs = bufs
-    (iptr,) = uploader(dev).upload(np.asarray(local_ids, dtype=np.int32))
+        bufs = store._train_bufs = TrainBuffers(store)
+    (iptr,) = rt.desc.put(np.asarray(local_ids, dtype=np.int32))
+    tptr, trk = rt.out.take(np.float64, k * hp.epochs * 2)
+    trk[:] = np.nan
+    eptr, er = rt.out.take(np.int32, k)
+    bptr, be = rt.out.take(np.int32, k)
     a = TrainArgs()
     a.params = store.params.data_ptr()
     a.adam_m = store.adam_m.data_ptr()
@@ -433,22 +379,20 @@ def train(store, local_ids: Sequence[int], hp, dims, bufs: Optional[TrainBuffers
     a.valid_x = store.valid.data_ptr()
     a.valid_off = bufs.valid_off.data_ptr()
     a.client_idx = iptr
-    # tracking rows are written with stride hp.epochs
-    trk = bufs.tracking.view(-1)[:k * hp.epochs * 2].view(k, hp.epochs, 2)
-    a.tracking = trk.data_ptr()
-    a.epochs_run = bufs.epochs_run.data_ptr()
-    a.best_epoch = bufs.best_epoch.data_ptr()
+    a.tracking = tptr
+    a.epochs_run = eptr
+    a.best_epoch = bptr
     a.epochs = hp.epochs
     a.batch = hp.batch_size
     a.patience = hp.patience
     a.d_in, a.hidden, a.latent = dims.d_in, dims.hidden, dims.latent
     a.lr, a.beta1, a.beta2, a.eps = hp.lr, hp.beta1, hp.beta2, hp.eps
     a.lam, a.mu = hp.shrink_lambda, hp.fedprox_mu
-    rc = lib().fedmx_train(ctypes.byref(a), k, _stream(dev))
+    rc = lib().fedmx_train(ctypes.byref(a), k, rt.stream)
     if rc == -2:
         raise ValueError(f"fused training kernel supports batch sizes 1..16, got {hp.batch_size}")
     _check(rc, "fedmx_train")
-    return trk, bufs.epochs_run[:k], bufs.best_epoch[:k]
+    return trk.reshape(k, hp.epochs, 2), er, be
 
 
 def probe_mfma(device) -> np.ndarray:

@@ -1,0 +1,151 @@
+"""Minimal HIP runtime binding for the host-side hot path.
+
+Per-round protocol traffic is tiny (descriptor arrays of a few hundred bytes
+down, a few scores up), so its cost is API overhead, not bandwidth.  Instead
+of staging copies through torch (dispatcher + hipMemcpyAsync + events, tens
+of microseconds each), the framework keeps two rings of *mapped, coherent*
+pinned host memory:
+
+* ``DescRing`` – the host writes descriptor arrays with a plain numpy copy and
+  passes the ring's *device* address to the kernel, which reads them over
+  PCIe at block start (zero copy, no API call);
+* ``OutRing``  – kernels write host-visible results (scores, drifts, AUCs,
+  training tracking) straight into it; the host reads them after the single
+  ``hipStreamSynchronize`` that ends each protocol phase.
+
+A ring region is reused only after a stream synchronisation that follows its
+last use (``generation`` bookkeeping), so the host never overwrites bytes a
+queued kernel has yet to read.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+hipHostMallocMapped = 0x2
+hipHostMallocCoherent = 0x40000000
+
+_lib = None
+_lock = threading.Lock()
+
+
+def rt():
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                L = None
+                for name in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+                    try:
+                        L = ctypes.CDLL(name)
+                        break
+                    except OSError:
+                        continue
+                if L is None:
+                    raise OSError("libamdhip64.so not found")
+                vp = ctypes.c_void_p
+                L.hipHostMalloc.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_uint]
+                L.hipHostMalloc.restype = ctypes.c_int
+                L.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(vp), vp, ctypes.c_uint]
+                L.hipHostGetDevicePointer.restype = ctypes.c_int
+                L.hipStreamSynchronize.argtypes = [vp]
+                L.hipStreamSynchronize.restype = ctypes.c_int
+                L.hipHostFree.argtypes = [vp]
+                L.hipHostFree.restype = ctypes.c_int
+                _lib = L
+    return _lib
+
+
+def stream_sync(stream: int) -> None:
+    rc = rt().hipStreamSynchronize(ctypes.c_void_p(stream))
+    if rc != 0:
+        raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
+    SyncClock.tick()
+
+
+class SyncClock:
+    """Counts completed stream synchronisations (ring-reuse generations)."""
+
+    gen = 0
+
+    @classmethod
+    def tick(cls):
+        cls.gen += 1
+
+
+class MappedBuffer:
+    def __init__(self, nbytes: int):
+        L = rt()
+        hp = ctypes.c_void_p()
+        rc = L.hipHostMalloc(ctypes.byref(hp), nbytes, hipHostMallocMapped | hipHostMallocCoherent)
+        if rc != 0:
+            raise RuntimeError(f"hipHostMalloc({nbytes}) failed ({rc})")
+        dp = ctypes.c_void_p()
+        rc = L.hipHostGetDevicePointer(ctypes.byref(dp), hp, 0)
+        if rc != 0:
+            raise RuntimeError(f"hipHostGetDevicePointer failed ({rc})")
+        self.host_ptr = hp.value
+        self.dev_ptr = dp.value
+        self.nbytes = nbytes
+        self.np = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.host_ptr))
+
+    def view(self, off: int, dtype, count: int) -> np.ndarray:
+        return self.np[off:off + count * np.dtype(dtype).itemsize].view(dtype)
+
+    def __del__(self):
+        try:
+            if self.host_ptr:
+                # queued kernels may still target this memory: drain first
+                if _lib is not None:
+                    _lib.hipDeviceSynchronize()
+                    _lib.hipHostFree(ctypes.c_void_p(self.host_ptr))
+                self.host_ptr = None
+        except Exception:
+            pass
+
+
+class _Ring:
+    def __init__(self, nbytes: int, stream: int):
+        self.buf = MappedBuffer(nbytes)
+        self.stream = stream
+        self.off = 0
+        self.wrap_gen = -1   # generation at which the current pass started
+
+    def _alloc(self, nbytes: int) -> int:
+        nbytes = (nbytes + 63) & ~63
+        if nbytes > self.buf.nbytes:
+            raise ValueError(f"ring request of {nbytes} B exceeds ring size {self.buf.nbytes}")
+        if self.off + nbytes > self.buf.nbytes:
+            # wrapping: earlier regions may still be read/written by queued kernels
+            # unless a stream synchronisation happened since this pass began
+            if SyncClock.gen <= self.wrap_gen:
+                stream_sync(self.stream)
+            self.off = 0
+            self.wrap_gen = SyncClock.gen
+        o = self.off
+        self.off += nbytes
+        return o
+
+
+class DescRing(_Ring):
+    def put(self, *arrays: np.ndarray) -> List[int]:
+        blobs = [np.ascontiguousarray(a).view(np.uint8).reshape(-1) for a in arrays]
+        sizes = [(b.nbytes + 63) & ~63 for b in blobs]
+        o = self._alloc(sum(sizes))
+        ptrs = []
+        for b, s in zip(blobs, sizes):
+            self.buf.np[o:o + b.nbytes] = b
+            ptrs.append(self.buf.dev_ptr + o)
+            o += s
+        return ptrs
+
+
+class OutRing(_Ring):
+    def take(self, dtype, count: int):
+        """Reserve ``count`` elements; returns (device address, host numpy view)."""
+        nb = int(count) * np.dtype(dtype).itemsize
+        o = self._alloc(max(nb, 1))
+        return self.buf.dev_ptr + o, self.buf.view(o, dtype, int(count))

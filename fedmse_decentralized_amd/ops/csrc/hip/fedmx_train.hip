@@ -84,6 +84,51 @@ __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float 
 #endif
 }
 
+// Four elements (one accumulator register quad) at a time with packed fp32
+// math (v_pk_fma/mul/add_f32: two lanes' elements per instruction issue), the
+// transcendental sqrt/rcp per element.  Same operation order as adam_update.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <bool PROX>
+__device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4], const float (&a)[4], f32x4 g,
+                                      const AdamStep& K, float& prox_acc) {
+#if FEDMX_EXACT_ADAM
+#pragma unroll
+  for (int r = 0; r < 4; ++r) adam_update<PROX>(p[r], m[r], v[r], a[r], g[r], K, prox_acc);
+#else
+  const f32x2 c1 = {K.one_m_b1, K.one_m_b1}, b2 = {K.b2, K.b2}, c2 = {K.one_m_b2, K.one_m_b2};
+  const f32x2 ib = {K.inv_bc2s, K.inv_bc2s}, ep = {K.eps, K.eps}, ns = {K.neg_step_size, K.neg_step_size};
+  f32x2 pacc = {0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    f32x2 pp = {p[2 * h], p[2 * h + 1]};
+    f32x2 mm = {m[2 * h], m[2 * h + 1]};
+    f32x2 vv = {v[2 * h], v[2 * h + 1]};
+    f32x2 gg = {g[2 * h], g[2 * h + 1]};
+    if (PROX) {
+      const f32x2 aa = {a[2 * h], a[2 * h + 1]};
+      const f32x2 tm = {K.two_mu, K.two_mu};
+      const f32x2 dp = pp - aa;
+      pacc = __builtin_elementwise_fma(dp, dp, pacc);
+      gg = __builtin_elementwise_fma(tm, dp, gg);
+    }
+    mm = __builtin_elementwise_fma(c1, gg - mm, mm);
+    vv = __builtin_elementwise_fma(c2 * gg, gg, vv * b2);
+    f32x2 den = {__builtin_amdgcn_sqrtf(vv.x), __builtin_amdgcn_sqrtf(vv.y)};
+    den = __builtin_elementwise_fma(den, ib, ep);
+    const f32x2 rr = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+    pp = __builtin_elementwise_fma(ns, mm * rr, pp);
+    p[2 * h] = pp.x;
+    p[2 * h + 1] = pp.y;
+    m[2 * h] = mm.x;
+    m[2 * h + 1] = mm.y;
+    v[2 * h] = vv.x;
+    v[2 * h + 1] = vv.y;
+  }
+  if (PROX) prox_acc += pacc.x + pacc.y;
+#endif
+}
+
 // LDS plan (floats); total < 160 KiB -> one workgroup per CU.
 constexpr int L_W1 = HP * S_W1;          // 4224  shared, column block per wave
 constexpr int L_W4 = DP * S_W4;          // 4608  shared, row block per wave
@@ -479,13 +524,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
           g10 = mfma16(a1[s], b0[s], g10);
           g11 = mfma16(a1[s], b1[s], g11);
         }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          adam_update<PROX>(P.q4[0][0][r], M.q4[0][0][r], V.q4[0][0][r], PROX ? AN.q4[0][0][r] : 0.f, g00[r], K, prox_acc);
-          adam_update<PROX>(P.q4[0][1][r], M.q4[0][1][r], V.q4[0][1][r], PROX ? AN.q4[0][1][r] : 0.f, g01[r], K, prox_acc);
-          adam_update<PROX>(P.q4[1][0][r], M.q4[1][0][r], V.q4[1][0][r], PROX ? AN.q4[1][0][r] : 0.f, g10[r], K, prox_acc);
-          adam_update<PROX>(P.q4[1][1][r], M.q4[1][1][r], V.q4[1][1][r], PROX ? AN.q4[1][1][r] : 0.f, g11[r], K, prox_acc);
-        }
+adam4<PROX>(P.q4[0][0], M.q4[0][0], V.q4[0][0], AN.q4[0][0], g00, K, prox_acc);
+        adam4<PROX>(P.q4[0][1], M.q4[0][1], V.q4[0][1], AN.q4[0][1], g01, K, prox_acc);
+        adam4<PROX>(P.q4[1][0], M.q4[1][0], V.q4[1][0], AN.q4[1][0], g10, K, prox_acc);
+        adam4<PROX>(P.q4[1][1], M.q4[1][1], V.q4[1][1], AN.q4[1][1], g11, K, prox_acc);
       }
       // ---- stage X^T, H1^T, Z^T for the remaining weight gradients
 #pragma unroll
@@ -558,8 +600,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         f32x4 acc = zero4();
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) adam_update<PROX>(P.o[r], M.o[r], V.o[r], PROX ? AN.o[r] : 0.f, acc[r], K, prox_acc);
+        adam4<PROX>(P.o, M.o, V.o, AN.o, acc, K, prox_acc);
       }
       // ---- dW1 (own columns) = dH1^T X + fused Adam
       {
@@ -575,13 +616,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
           g10 = mfma16(a1[s], b0[s], g10);
           g11 = mfma16(a1[s], b1[s], g11);
         }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          adam_update<PROX>(P.q1[0][0][r], M.q1[0][0][r], V.q1[0][0][r], PROX ? AN.q1[0][0][r] : 0.f, g00[r], K, prox_acc);
-          adam_update<PROX>(P.q1[0][1][r], M.q1[0][1][r], V.q1[0][1][r], PROX ? AN.q1[0][1][r] : 0.f, g01[r], K, prox_acc);
-          adam_update<PROX>(P.q1[1][0][r], M.q1[1][0][r], V.q1[1][0][r], PROX ? AN.q1[1][0][r] : 0.f, g10[r], K, prox_acc);
-          adam_update<PROX>(P.q1[1][1][r], M.q1[1][1][r], V.q1[1][1][r], PROX ? AN.q1[1][1][r] : 0.f, g11[r], K, prox_acc);
-        }
+adam4<PROX>(P.q1[0][0], M.q1[0][0], V.q1[0][0], AN.q1[0][0], g00, K, prox_acc);
+        adam4<PROX>(P.q1[0][1], M.q1[0][1], V.q1[0][1], AN.q1[0][1], g01, K, prox_acc);
+        adam4<PROX>(P.q1[1][0], M.q1[1][0], V.q1[1][0], AN.q1[1][0], g10, K, prox_acc);
+        adam4<PROX>(P.q1[1][1], M.q1[1][1], V.q1[1][1], AN.q1[1][1], g11, K, prox_acc);
       }
       if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
       // publish the updated parameters (own W1 columns / W4 rows / small tile)

@@ -58,17 +58,19 @@ class Verifier:
             return VerifyDecision(True, 0.0, 0.0)
         change = perf_new - st.history_perf
         st.history_version, st.history_perf, st.history_round = version, perf_new, current_round
-        log.info(f"Client {client_id} - Param changes: {drift:.10f}, Performance change: {change:.10f}")
-        log.info(f"Using {self.method} dataset for verification")
+        if log.isEnabledFor(logging.INFO):
+            log.info(f"Client {client_id} - Param changes: {drift:.10f}, Performance change: {change:.10f}")
+            log.info(f"Using {self.method} dataset for verification")
         ok = (drift <= self.thr) and (change >= -self.perf_thr)
         return VerifyDecision(ok, change, drift)
 
     def apply(self, client_id: int, st: VerifierState, dec: VerifyDecision) -> None:
         if dec.verified:
             st.rejected_updates = 0
-            log.info(f"[Client {client_id}] Model verified and updated. Performance change: {dec.perf_change:.10f}")
+            if log.isEnabledFor(logging.INFO):
+                log.info(f"[Client {client_id}] Model verified and updated. Performance change: {dec.perf_change:.10f}")
         else:
             st.rejected_updates += 1
-            log.warning(f"[Client {client_id}] Model update rejected. Performance change: {dec.perf_change:.10f}")
+            log.warning("[Client %d] Model update rejected. Performance change: %.10f", client_id, dec.perf_change)
             if st.rejected_updates >= self.max_rejected:
                 log.error(f"[Client {client_id}] Too many rejected updates. Possible attack detected.")

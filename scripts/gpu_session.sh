@@ -28,7 +28,7 @@ if [ "$MODE" = all ] || [ "$MODE" = kernels ]; then
   step bench_kernels 300 python scripts/bench_kernels.py
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
-  step bench 300 python bench.py --steps 20 --warmup 3 --out "$OUT/bench.json"
+  step bench 300 python bench.py --steps 20 --warmup 3 --out "$OUT/bench.json" --profile "$OUT/bench_profile.txt"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp && export TMPDIR=/tmp
