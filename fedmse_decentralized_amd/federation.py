@@ -168,6 +168,9 @@ class Federation:
             shrink_lambda=float(cfg.shrink_lambda) if self.model_type == "hybrid" else 0.0,
             fedprox_mu=cfg.fedprox_mu if self.update_type == "fedprox" else 0.0,
             patience=cfg.global_patience)
+        from .models.layout import padded_index
+
+        self._canon_idx = padded_index(self.dims)[0].numpy()
         self.save_dirs = {c: cfg.client_save_dir(self.run, self.model_type, self.update_type, clients[c].name)
                           for c in self.local}
         if cfg.save_checkpoints:
@@ -222,6 +225,7 @@ class Federation:
         st = self.engine.store
         snap, ev = snapshot_to_host(st.best)
         dims = self.dims
+        cidx = self._canon_idx
         for i, c in enumerate(local_sel):
             d = self.save_dirs[c]
             row = self._loc(c)
@@ -230,7 +234,7 @@ class Federation:
 
             def job(d=d, row=row, improved=improved, trk=trk):
                 if improved:
-                    ckpt.save_model_cpt(d, snap[row], dims)
+                    ckpt.save_model_cpt_fast(d, snap[row].numpy()[cidx], dims)
                 ckpt.save_tracking(d, trk)
             self.writer.submit(job, ev)
 
@@ -280,11 +284,12 @@ class Federation:
                 with self.tel.phase("io"):
                     self._write_checkpoints(res, local_sel)
         log.info("Starting voting for aggregator...")
-        vec = torch.zeros(N, 3, dtype=torch.float64)
-        for i, c in enumerate(local_sel):
-            vec[c, 0] = float(scores_np[i, 0])
-            vec[c, 1] = float(scores_np[i, 1]) if need_dev else 0.0
-            vec[c, 2] = epochs_local.get(c, 0)
+        vec = np.zeros((N, 3), dtype=np.float64)
+        if local_sel:
+            ls = np.asarray(local_sel)
+            vec[ls, 0] = scores_np[:, 0]
+            vec[ls, 1] = scores_np[:, 1] if need_dev else 0.0
+            vec[ls, 2] = [epochs_local.get(c, 0) for c in local_sel]
         with self.tel.phase("comm"):
             vec = self.comm.all_reduce_sum(vec)
         with self.tel.phase("vote"):
@@ -332,11 +337,11 @@ class Federation:
         log.info("Calculating metrics for all models...")
         with self.tel.phase("eval"):
             er = eng.evaluate(self.model_type, cfg.metric, keep_latents=cfg.save_latents)
-            vec = torch.zeros(N, dtype=torch.float64)
-            vec[self.local[0]:self.local[-1] + 1] = torch.from_numpy(np.asarray(er.metrics, dtype=np.float64))
+            vec = np.zeros(N, dtype=np.float64)
+            vec[self.local[0]:self.local[-1] + 1] = er.metrics
         with self.tel.phase("comm"):
             vec = self.comm.all_reduce_sum(vec)
-        metrics = vec.numpy().copy()
+        metrics = np.array(vec, dtype=np.float64)
         self.noise.iterators(N * (2 if self.model_type == "hybrid" else 1))
         if info:
             for i in range(N):
@@ -382,7 +387,7 @@ class Federation:
         perf = {k: 1.0 / (1.0 + float(m)) for k, m in zip(keys, mse_np)}   # 1 / (1 + MSE)
         drift = {v: float(x) for v, x in zip(need, drift_np)}
         accept = []
-        vec = torch.zeros(N, 2, dtype=torch.float64)
+        vec = np.zeros((N, 2), dtype=np.float64)
         for c in receivers:
             vs_ = self.vstate[c]
             dr = drift.get(vs_.history_version, 0.0) if vs_.history_version is not None else 0.0

@@ -23,37 +23,38 @@ struct SegDesc {
 };
 static_assert(sizeof(SegDesc) == 24, "SegDesc layout is shared with Python");
 
+__device__ __forceinline__ double block_sum_d(double v, double* s_w) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lane == 0) s_w[wv] = v;
+  __syncthreads();
+  const double r = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  __syncthreads();
+  return r;
+}
+
+// One workgroup per segment; batches are reduced one after another with all
+// 256 threads striding over the batch's rows (a 6.7K-row dev segment is one
+// batch: 26 loads per thread + one block reduction).
 __global__ __launch_bounds__(256) void score_reduce_kernel(const SegDesc* __restrict__ descs, int d_in) {
   const SegDesc d = descs[blockIdx.x];
-  __shared__ double s_tot[256];
-  __shared__ double s_vote[256];
+  __shared__ double s_w[4];
   const int tid = threadIdx.x;
   const int bs = d.batch > 0 ? d.batch : (d.n > 0 ? d.n : 1);
   const int nb = (d.n + bs - 1) / bs;
-  // thread t accumulates whole rows; batch means need per-batch sums: each thread
-  // owns batches t, t+256, ... and sums their rows (batches are contiguous).
   double vote = 0.0, tot = 0.0;
-  for (int b = tid; b < nb; b += blockDim.x) {
+  for (int b = 0; b < nb; ++b) {
     const int r0 = b * bs;
     const int r1 = min(d.n, r0 + bs);
     double s = 0.0;
-    for (int r = r0; r < r1; ++r) s += (double)d.sse[r];
+    for (int r = r0 + tid; r < r1; r += blockDim.x) s += (double)d.sse[r];
+    s = block_sum_d(s, s_w);
     tot += s;
     vote += s / ((double)(r1 - r0) * d_in);
   }
-  s_tot[tid] = tot;
-  s_vote[tid] = vote;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) {
-      s_tot[tid] += s_tot[tid + o];
-      s_vote[tid] += s_vote[tid + o];
-    }
-    __syncthreads();
-  }
   if (tid == 0) {
-    d.out[0] = nb > 0 ? s_vote[0] / nb : __builtin_inf();
-    d.out[1] = d.n > 0 ? s_tot[0] / ((double)d.n * d_in) : __builtin_nan("");
+    d.out[0] = nb > 0 ? vote / nb : __builtin_inf();
+    d.out[1] = d.n > 0 ? tot / ((double)d.n * d_in) : __builtin_nan("");
   }
 }
 

@@ -56,6 +56,20 @@ class Comm:
         raise NotImplementedError
 
 
+def _np_wrap(fn):
+    """Let a tensor collective also take / return numpy arrays (host protocol vectors)."""
+    import functools
+
+    import numpy as np
+
+    @functools.wraps(fn)
+    def w(self, t, *a, **k):
+        if isinstance(t, np.ndarray):
+            return fn(self, torch.from_numpy(np.ascontiguousarray(t)), *a, **k).numpy()
+        return fn(self, t, *a, **k)
+    return w
+
+
 class LoopbackComm(Comm):
     def __init__(self, device: Optional[torch.device] = None):
         self.rank = 0
@@ -66,7 +80,7 @@ class LoopbackComm(Comm):
         return t
 
     def all_gather(self, t):
-        return t.unsqueeze(0)
+        return t[None] if not isinstance(t, torch.Tensor) else t.unsqueeze(0)
 
     def broadcast(self, t, src):
         return t
@@ -104,6 +118,7 @@ class ThreadComm(Comm):
         self.g.barrier.wait()
         return out
 
+    @_np_wrap
     def all_reduce_sum(self, t):
         parts = self._exchange(t.detach().cpu().clone())
         acc = parts[0].clone()
@@ -145,6 +160,7 @@ class TorchDistComm(Comm):
     def _to(self, t):
         return t if t.device == self.device else t.to(self.device)
 
+    @_np_wrap
     def all_reduce_sum(self, t):
         x = self._to(t).clone()
         self.dist.all_reduce(x, op=self.dist.ReduceOp.SUM)

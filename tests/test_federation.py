@@ -156,3 +156,21 @@ def test_global_early_stop_compat(tmp_path):
     fed = Federation(cfg, "hybrid", "avg", 0).setup()
     fed.run_all()
     assert fed.round_idx < 10   # AUC compared like a loss stops early (Q8)
+
+
+def test_fast_model_cpt_writer(tmp_path):
+    from fedmse_decentralized_amd.io.checkpoint import save_model_cpt_fast
+    from fedmse_decentralized_amd.models.layout import state_dict_to_canonical
+    from fedmse_decentralized_amd.models.reference import ReferenceSAE
+
+    m = ReferenceSAE()
+    ref = tmp_path / "ref.cpt"
+    torch.save(m.state_dict(), ref, _use_new_zipfile_serialization=False)
+    p = save_model_cpt_fast(str(tmp_path / "fast"), state_dict_to_canonical(m.state_dict()).numpy())
+    assert os.path.getsize(p) == os.path.getsize(ref)
+    a = torch.load(p, weights_only=True)
+    b = torch.load(ref, weights_only=True)
+    assert list(a) == list(b) and all(torch.equal(a[k], b[k]) for k in a)
+    assert open(p, "rb").read() == open(save_model_cpt_fast(str(tmp_path / "again"),
+                                                           state_dict_to_canonical(m.state_dict()).numpy()),
+                                         "rb").read()
