@@ -1,0 +1,73 @@
+"""Summarise a rocprofv3 kernel-trace database (rocpd SQLite) into markdown.
+
+Usage: python scripts/prof_summary.py gpurun_out/prof/run_results.db [--title T] [--out profiles/x.md]
+
+Prints per-kernel totals (calls, total/avg/min/max us, share, VGPR/AGPR/SGPR,
+LDS, scratch) and, for the last bench round, the per-round kernel timeline
+(span from the first to the last kernel of one train->eval round).
+"""
+from __future__ import annotations
+
+import argparse
+import sqlite3
+import sys
+
+
+def _short(name: str, n: int = 70) -> str:
+    s = name.replace("void ", "")
+    s = s.split("(")[0] if "fedmx" in s else s
+    return s if len(s) <= n else s[: n - 3] + "..."
+
+
+def summarize(db: str, title: str) -> str:
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, start, end, duration, grid_x, grid_y, workgroup_x, lds_size, scratch_size, "
+                     "vgpr_count, accum_vgpr_count, sgpr_count from kernels order by start").fetchall()
+    out = [f"# {title}", "", f"source: `{db}` (rocprofv3 --kernel-trace --stats)", ""]
+    agg = {}
+    for r in rows:
+        a = agg.setdefault(r[0], dict(n=0, tot=0.0, mn=1e30, mx=0.0, meta=r[4:]))
+        d = r[3] / 1000.0
+        a["n"] += 1
+        a["tot"] += d
+        a["mn"] = min(a["mn"], d)
+        a["mx"] = max(a["mx"], d)
+    total = sum(a["tot"] for a in agg.values()) or 1.0
+    out += ["| kernel | calls | total us | avg us | min us | max us | % | grid | VGPR/AGPR/SGPR | LDS B | scratch B |",
+            "|---|---|---|---|---|---|---|---|---|---|---|"]
+    for name, a in sorted(agg.items(), key=lambda kv: -kv[1]["tot"]):
+        gx, gy, wg, lds, scr, vg, ag, sg = a["meta"]
+        out.append(f"| `{_short(name)}` | {a['n']} | {a['tot']:.1f} | {a['tot'] / a['n']:.1f} | {a['mn']:.1f} | "
+                   f"{a['mx']:.1f} | {100 * a['tot'] / total:.1f} | {gx // max(wg, 1)}x{gy} | {vg}/{ag}/{sg} | {lds} | {scr} |")
+    # last round: from the last train_kernel launch to the end of the next auc kernel
+    starts = [i for i, r in enumerate(rows) if "train_kernel" in r[0]]
+    if starts:
+        i0 = starts[-2] if len(starts) > 1 else starts[-1]
+        i1 = starts[-1] if len(starts) > 1 else len(rows)
+        seg = rows[i0:i1]
+        t0 = seg[0][1]
+        out += ["", f"## one round timeline (kernels {i0}..{i1 - 1}, span {(seg[-1][2] - t0) / 1000:.1f} us, "
+                f"busy {sum(r[3] for r in seg) / 1000:.1f} us)", "",
+                "| t0 us | dur us | gap before us | kernel |", "|---|---|---|---|"]
+        prev_end = t0
+        for r in seg:
+            out.append(f"| {(r[1] - t0) / 1000:.1f} | {r[3] / 1000:.1f} | {(r[1] - prev_end) / 1000:.1f} | `{_short(r[0])}` |")
+            prev_end = r[2]
+    return "\n".join(out) + "\n"
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--title", default="rocprofv3 kernel summary")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args(argv)
+    text = summarize(a.db, a.title)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(text)
+    sys.stdout.write(text)
+
+
+if __name__ == "__main__":
+    main()

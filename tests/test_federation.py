@@ -167,7 +167,8 @@ def test_fast_model_cpt_writer(tmp_path):
     ref = tmp_path / "ref.cpt"
     torch.save(m.state_dict(), ref, _use_new_zipfile_serialization=False)
     p = save_model_cpt_fast(str(tmp_path / "fast"), state_dict_to_canonical(m.state_dict()).numpy())
-    assert os.path.getsize(p) == os.path.getsize(ref)
+    # sizes may differ by a few bytes: legacy storage keys are decimal addresses
+    assert abs(os.path.getsize(p) - os.path.getsize(ref)) <= 64
     a = torch.load(p, weights_only=True)
     b = torch.load(ref, weights_only=True)
     assert list(a) == list(b) and all(torch.equal(a[k], b[k]) for k in a)
