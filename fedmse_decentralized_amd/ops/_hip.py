@@ -17,7 +17,9 @@ never a silent PyTorch fallback.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
+from pathlib import Path
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -58,6 +60,7 @@ class TrainArgs(ctypes.Structure):
         ("d_in", ctypes.c_int32), ("hidden", ctypes.c_int32), ("latent", ctypes.c_int32),
         ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
         ("eps", ctypes.c_float), ("lam", ctypes.c_float), ("mu", ctypes.c_float),
+        ("stamps", ctypes.c_void_p),
     ]
 
 
@@ -67,8 +70,9 @@ def lib():
         return _lib
     with _lock:
         if _lib is None:
-            path = build.HIP_LIB
-            if not path.exists():
+            override = os.environ.get("FEDMX_HIP_LIB")
+            path = Path(override) if override else build.HIP_LIB
+            if not path.exists() and not override:
                 build.build_hip()   # hipcc cross-compiles for gfx950 in-tree
             L = ctypes.CDLL(str(path))
             vp, i32 = ctypes.c_void_p, ctypes.c_int
@@ -352,7 +356,7 @@ class TrainBuffers:
         self.valid_off = torch.from_numpy(store.valid_off).to(dev)
 
 
-def train(store, local_ids: Sequence[int], hp, dims):
+def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tensor] = None):
     """Launch the fused training kernel for store rows ``local_ids`` (async).
     Returns host views (tracking[k, E, 2], epochs_run[k], best_epoch[k])
     written by the kernel, valid after the next stream sync."""
@@ -388,6 +392,7 @@ def train(store, local_ids: Sequence[int], hp, dims):
     a.d_in, a.hidden, a.latent = dims.d_in, dims.hidden, dims.latent
     a.lr, a.beta1, a.beta2, a.eps = hp.lr, hp.beta1, hp.beta2, hp.eps
     a.lam, a.mu = hp.shrink_lambda, hp.fedprox_mu
+    a.stamps = stamps.data_ptr() if stamps is not None else None
     rc = lib().fedmx_train(ctypes.byref(a), k, rt.stream)
     if rc == -2:
         raise ValueError(f"fused training kernel supports batch sizes 1..16, got {hp.batch_size}")

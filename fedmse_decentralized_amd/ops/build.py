@@ -23,6 +23,7 @@ CSRC = HERE / "csrc"
 LIBDIR = HERE / "lib"
 HOST_LIB = LIBDIR / "libfedmx_host.so"
 HIP_LIB = LIBDIR / "libfedmx_hip.so"
+HIP_STAMPS_LIB = LIBDIR / "libfedmx_hip_stamps.so"
 OFFLOAD_ARCH = os.environ.get("FEDMX_OFFLOAD_ARCH", "gfx950")
 
 
@@ -72,22 +73,25 @@ def hipcc_path() -> str:
     return p
 
 
-def build_hip(force: bool = False, verbose: bool = False, extra_flags=()) -> Path:
+def build_hip(force: bool = False, verbose: bool = False, extra_flags=(), target: Path = HIP_LIB) -> Path:
+    """``extra_flags``/``target`` build variants next to the main library, e.g.
+    the in-kernel timestamp build ``-DFEDMX_STAMPS=1`` -> ``libfedmx_hip_stamps.so``
+    (selected at load time with ``FEDMX_HIP_LIB``)."""
     srcs = _sources("hip", (".hip",))
-    if not force and not _stale(HIP_LIB, srcs + _headers()):
-        return HIP_LIB
+    if not force and not _stale(target, srcs + _headers()):
+        return target
     LIBDIR.mkdir(parents=True, exist_ok=True)
-    tmp = HIP_LIB.with_suffix(".so.tmp")
+    tmp = target.with_suffix(".so.tmp")
     # -ffp-contract=off: separately rounded mul/add like the torch ops the kernels
     # reproduce (aggregation sums are then bit-identical to the reference order)
     cmd = [hipcc_path(), f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-munsafe-fp-atomics", f"-I{CSRC / 'hip'}", *extra_flags, *map(str, srcs),
            "-o", str(tmp)]
     out = _run(cmd)
-    os.replace(tmp, HIP_LIB)
+    os.replace(tmp, target)
     if verbose:
         print(out, end="")
-    return HIP_LIB
+    return target
 
 
 def build_all(force: bool = False, verbose: bool = False):

@@ -53,7 +53,27 @@ struct TrainArgs {
   int32_t* best_epoch;      // [k]
   int32_t epochs, batch, patience, d_in, hidden, latent;
   float lr, beta1, beta2, eps, lambda, mu;
+  uint64_t* stamps;         // [4 waves][32] s_memtime stamps of one step (FEDMX_STAMPS builds), or null
 };
+
+// In-kernel phase timestamps (build with -DFEDMX_STAMPS=1): wave w's lane 0 of
+// workgroup 0 records s_memtime at fixed points of training step STAMP_STEP
+// of epoch 0 and of the first validation batch.
+#ifndef FEDMX_STAMPS
+#define FEDMX_STAMPS 0
+#endif
+constexpr int STAMP_STEP = 20;
+#if FEDMX_STAMPS
+#define STAMP(cond, i)                                                                          \
+  do {                                                                                          \
+    if ((cond) && A.stamps != nullptr && blockIdx.x == 0 && lane == 0)                          \
+      A.stamps[w * 32 + (i)] = __builtin_amdgcn_s_memtime();                                   \
+  } while (0)
+#else
+#define STAMP(cond, i) \
+  do {                 \
+  } while (0)
+#endif
 
 struct AdamStep {
   float one_m_b1, b2, one_m_b2, inv_bc2s, bc2s, eps, neg_step_size, two_mu;
@@ -280,6 +300,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   const int d_in = A.d_in, hidden = A.hidden, latent = A.latent;
 
   // ---- load client state: global -> LDS masters -> owned registers ----------
+  STAMP(true, 28);
   Slab P, M, V, AN;
   global_to_masters(Mg, sW1, sW4, sW2, sW3);
   __syncthreads();
@@ -298,6 +319,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   global_to_masters(Pg, sW1, sW4, sW2, sW3);
   __syncthreads();
   lds_to_slab(P, L);   // masters keep the live parameters from here on
+  STAMP(true, 29);
 
   const int B = A.batch;
   const float* const Xtr = A.train_x + (size_t)A.train_off[cid] * DP;
@@ -320,6 +342,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
     fm1[r] = (xcol + 16 + r < d_in) ? 1.f : 0.f;
   }
 
+  bool stamp_fwd = false;
+  (void)stamp_fwd;
   auto load_x = [&](const float* X, int row0, int bcur, f32x4& x0, f32x4& x1) {
     const bool ok = c < bcur;
     const float* src = X + (size_t)(row0 + c) * DP + xcol;
@@ -334,6 +358,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   auto forward = [&](const f32x4& x0, const f32x4& x1, int bcur, f32x4 (&h1)[2], f32x4& z, f32x4& zb,
                      f32x4 (&h3)[2], f32x4 (&y)[2], float& norm_c, double& lacc) {
     float* red = sRedH1 + parity * L_RED;
+    const bool sf = stamp_fwd;
     {
       f32x4 acc0 = zero4(), acc1 = zero4();
       const f32x4 a00 = lds_read4(a1p);
@@ -353,7 +378,9 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       lds_write4(red + (w * 2 + 0) * 256 + lane * 4, acc0);
       lds_write4(red + (w * 2 + 1) * 256 + lane * 4, acc1);
     }
+    STAMP(sf, 1);
     __syncthreads();  // barrier #1
+    STAMP(sf, 2);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       f32x4 s = lds_read4(red + t * 256 + lane * 4);
@@ -462,7 +489,11 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       const int bcur = min(B, n_tr - row0);
       f32x4 h1[2], z, zb, h3[2], y[2];
       float norm_c;
+      const bool stamp_on = (ep == 0 && bi == STAMP_STEP);
+      STAMP(stamp_on, 0);
+      stamp_fwd = FEDMX_STAMPS && stamp_on;
       forward(xa, xb, bcur, h1, z, zb, h3, y, norm_c, acc_tr);
+      STAMP(stamp_on, 3);
       if (bi + 1 < nb) load_x(Xtr, row0 + B, min(B, n_tr - row0 - B), na, nbx);  // prefetch
 
       // current W2a / W3a (all tiles, D layout) for the backward-data products;
@@ -509,6 +540,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         lds_write4(redw, acc0);
         lds_write4(redw + 256, acc1);
       }
+      STAMP(stamp_on, 4);
       wave_sync();
       // ---- dW4 (own rows) + fused Adam
       {
@@ -529,6 +561,7 @@ adam4<PROX>(P.q4[0][0], M.q4[0][0], V.q4[0][0], AN.q4[0][0], g00, K, prox_acc);
         adam4<PROX>(P.q4[1][0], M.q4[1][0], V.q4[1][0], AN.q4[1][0], g10, K, prox_acc);
         adam4<PROX>(P.q4[1][1], M.q4[1][1], V.q4[1][1], AN.q4[1][1], g11, K, prox_acc);
       }
+      STAMP(stamp_on, 5);
       // ---- stage X^T, H1^T, Z^T for the remaining weight gradients
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -538,7 +571,9 @@ adam4<PROX>(P.q4[0][0], M.q4[0][0], V.q4[0][0], AN.q4[0][0], g00, K, prox_acc);
         sH1T[tw + (16 + r) * S_T] = h1[1][r];
         sZT[tw + r * S_T] = zb[r];
       }
+      STAMP(stamp_on, 6);
       __syncthreads();  // barrier #2: dH3 partials of all waves visible
+      STAMP(stamp_on, 7);
       f32x4 dh3[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -585,6 +620,7 @@ adam4<PROX>(P.q4[0][0], M.q4[0][0], V.q4[0][0], AN.q4[0][0], g00, K, prox_acc);
           sT1[tw + (16 + r) * S_T] = (h1i < hidden && h1[1][r] > 0.f) ? acc1[r] : 0.f;
         }
       }
+      STAMP(stamp_on, 8);
       wave_sync();
       // ---- owned small tile: w<2 -> dW3 tile (h-block w) = dH3^T Z ;
       //                        w>=2 -> dW2 tile (h-block w-2) = dZ^T H1
@@ -602,6 +638,7 @@ adam4<PROX>(P.q4[0][0], M.q4[0][0], V.q4[0][0], AN.q4[0][0], g00, K, prox_acc);
         for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
         adam4<PROX>(P.o, M.o, V.o, AN.o, acc, K, prox_acc);
       }
+      STAMP(stamp_on, 9);
       // ---- dW1 (own columns) = dH1^T X + fused Adam
       {
         const f32x4 a0 = lds_read4(sT1 + tr);
@@ -621,10 +658,12 @@ adam4<PROX>(P.q1[0][0], M.q1[0][0], V.q1[0][0], AN.q1[0][0], g00, K, prox_acc);
         adam4<PROX>(P.q1[1][0], M.q1[1][0], V.q1[1][0], AN.q1[1][0], g10, K, prox_acc);
         adam4<PROX>(P.q1[1][1], M.q1[1][1], V.q1[1][1], AN.q1[1][1], g11, K, prox_acc);
       }
+      STAMP(stamp_on, 10);
       if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
       // publish the updated parameters (own W1 columns / W4 rows / small tile)
       slab_to_lds(P, L);
       wave_sync();
+      STAMP(stamp_on, 11);
       xa = na;
       xb = nbx;
     }
@@ -635,11 +674,15 @@ adam4<PROX>(P.q1[0][0], M.q1[0][0], V.q1[0][0], AN.q1[0][0], g00, K, prox_acc);
       const int row0 = bi * B;
       const int bcur = min(B, n_va - row0);
       f32x4 va, vb;
+      STAMP(ep == 0 && bi == 1, 16);
       load_x(Xva, row0, bcur, va, vb);
       f32x4 h1[2], z, zb, h3[2], y[2];
       float norm_c;
+      STAMP(ep == 0 && bi == 1, 17);
       forward(va, vb, bcur, h1, z, zb, h3, y, norm_c, acc_va);
+      STAMP(ep == 0 && bi == 1, 18);
     }
+    STAMP(ep == 0, 12);
     double prox_now = 0.0;
     if (PROX) {
       float pr = 0.f;
@@ -693,9 +736,11 @@ adam4<PROX>(P.q1[0][0], M.q1[0][0], V.q1[0][0], AN.q1[0][0], g00, K, prox_acc);
       ++worse;
     }
     __syncthreads();  // sLoss reuse / masters stable for the snapshot copy
+    STAMP(ep == 0, 13);
     if (worse >= A.patience && worse > 0) break;
   }
 
+  STAMP(true, 30);
   // ---- write back: params (masters), then m and v through the same staging
   masters_to_global(Pg, sW1, sW4, sW2, sW3);
   __syncthreads();
@@ -711,6 +756,7 @@ adam4<PROX>(P.q1[0][0], M.q1[0][0], V.q1[0][0], AN.q1[0][0], g00, K, prox_acc);
     A.epochs_run[kslot] = ep_run;
     A.best_epoch[kslot] = best_ep;
   }
+  STAMP(true, 31);
 }
 
 }  // namespace fedmx

@@ -28,7 +28,11 @@ if [ "$MODE" = all ] || [ "$MODE" = kernels ]; then
   step bench_kernels 300 python scripts/bench_kernels.py
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
-  step bench 300 python bench.py --steps 20 --warmup 3 --out "$OUT/bench.json" --profile "$OUT/bench_profile.txt"
+  step bench 300 python bench.py --steps 50 --warmup 5 --out "$OUT/bench.json"
+  step bench_cprofile 300 python bench.py --steps 20 --warmup 3 --out "$OUT/bench_cprofile.json" --profile "$OUT/bench_profile.txt"
+fi
+if [ "$MODE" = stamps ]; then
+  step train_stamps 300 python scripts/train_stamps.py
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp && export TMPDIR=/tmp

@@ -1,0 +1,66 @@
+"""In-kernel phase timing of the fused training kernel (s_memtime stamps).
+
+Loads the ``-DFEDMX_STAMPS=1`` build (``libfedmx_hip_stamps.so``), trains the
+flagship round's 5 clients once and prints, per wave, the cycles spent in each
+phase of one training step (epoch 0, step STAMP_STEP), of one validation
+batch, and of the launch prologue / epilogue.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+ROOT = __file__.rsplit("/scripts/", 1)[0]
+sys.path.insert(0, ROOT)
+os.environ["FEDMX_HIP_LIB"] = os.path.join(ROOT, "fedmse_decentralized_amd/ops/lib/libfedmx_hip_stamps.so")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from fedmse_decentralized_amd.data.prepare import prepare_federation  # noqa: E402
+from fedmse_decentralized_amd.data.synthetic import SyntheticSpec, generate_federation  # noqa: E402
+from fedmse_decentralized_amd.engine.base import TrainHParams  # noqa: E402
+from fedmse_decentralized_amd.engine.hip_engine import HipEngine  # noqa: E402
+from fedmse_decentralized_amd.models.layout import DEFAULT_DIMS  # noqa: E402
+from fedmse_decentralized_amd.models.reference import init_client_params  # noqa: E402
+from fedmse_decentralized_amd.ops import _hip, build  # noqa: E402
+
+PHASES = [
+    (0, 1, "fwd L1 mfma + partial write"), (1, 2, "barrier #1"), (2, 3, "fwd reduce + L2..L4 + loss"),
+    (3, 4, "dY/transposes + dH3 partial"), (4, 5, "dW4 mfma + adam"), (5, 6, "stage X/H1/Z"),
+    (6, 7, "barrier #2"), (7, 8, "dH3 reduce + dZ + dH1"), (8, 9, "small tile mfma + adam"),
+    (9, 10, "dW1 mfma + adam"), (10, 11, "publish + wave_sync"), (0, 11, "TRAIN STEP TOTAL"),
+    (16, 17, "valid: load_x"), (17, 18, "valid: forward"), (28, 29, "prologue (state load)"),
+    (12, 13, "epoch end (reduce + snapshot)"), (30, 31, "epilogue (write back)"),
+]
+
+
+def main():
+    build.build_hip(extra_flags=["-DFEDMX_STAMPS=1"], target=build.HIP_STAMPS_LIB)
+    dev = torch.device("cuda", 0)
+    raws = generate_federation(SyntheticSpec(kind="nbaiot", n_clients=10, seed=1))
+    clients, _ = prepare_federation(raws, 1234)
+    init, _ = init_client_params(10, 0)
+    eng = HipEngine(DEFAULT_DIMS, dev)
+    eng.setup([c.train for c in clients], [c.valid for c in clients], [c.test for c in clients],
+              [c.test_label for c in clients], init)
+    hp = TrainHParams(epochs=5, batch_size=12, lr=1e-3, shrink_lambda=5.0, patience=10 ** 6)
+    stamps = torch.zeros(4 * 32, dtype=torch.int64, device=dev)
+    out = {}
+    for rep in range(3):
+        _hip.train(eng.store, list(range(5)), hp, eng.dims, stamps=stamps)
+        torch.cuda.synchronize()
+        st = stamps.view(4, 32).cpu().numpy().astype(np.int64)
+        res = {}
+        for a, b, name in PHASES:
+            res[name] = [int(st[w, b] - st[w, a]) if st[w, a] and st[w, b] else None for w in range(4)]
+        out[f"rep{rep}"] = res
+        stamps.zero_()
+    for name, v in out["rep2"].items():
+        print(f"{name:34s} " + " ".join(f"{x:8d}" if x is not None else "       -" for x in v))
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
