@@ -395,7 +395,7 @@ def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tens
     a.stamps = stamps.data_ptr() if stamps is not None else None
     rc = lib().fedmx_train(ctypes.byref(a), k, rt.stream)
     if rc == -2:
-        raise ValueError(f"fused training kernel supports batch sizes 1..16, got {hp.batch_size}")
+        raise ValueError(f"fused training kernel needs batch_size >= 1, got {hp.batch_size}")
     _check(rc, "fedmx_train")
     return trk.reshape(k, hp.epochs, 2), er, be
 

@@ -21,13 +21,23 @@
 //     redundantly by every wave from one shared LDS master, which owners
 //     update after barrier #2 and readers re-read after barrier #1 of the next
 //     step, so no extra synchronisation is needed.
-//   * Per training step: 2 workgroup barriers; per validation batch: 1.
-//   * Global memory is touched only to stream the batches (prefetched one step
-//     ahead) and, through LDS staging with coalesced 16-byte accesses, to load
-//     / store the client state and the best-validation snapshot.
-// All products run on v_mfma_f32_16x16x4_f32 (exact fp32).  Batch <= 16 rows
-// (reference default 12, src/main.py:52); padded batch columns and padded
-// features are masked out of the loss and every gradient.
+//   * W1 never goes through LDS during training: its owned block is kept in
+//     the MFMA A-operand layout, which is both what the layer-1 product reads
+//     and what the dW1^T = X^T dH1 product writes (dH1 is produced directly in
+//     the batch-major layout by swapping the operands of W2a^T dZ, and X is
+//     streamed in both layouts).
+//   * Batches of any size: a batch is processed as column tiles ("chunks") of
+//     16 rows; weight gradients accumulate in the MFMA accumulators over the
+//     chunks and Adam runs once per batch.  Per chunk: 2 workgroup barriers;
+//     per validation chunk: 1.
+//   * The layer-1 product of the next chunk is issued right after the W1 Adam
+//     update, ahead of the W4 / small-tile updates, so the MFMA pipe overlaps
+//     that optimizer VALU work.
+//   * Global memory is touched only to stream the batches (prefetched one
+//     chunk ahead) and, through LDS staging with coalesced 16-byte accesses, to
+//     load / store the client state and the best-validation snapshot.
+// All products run on v_mfma_f32_16x16x4_f32 (exact fp32).  Padded batch
+// columns and padded features are masked out of the loss and every gradient.
 #include "fedmx_common.h"
 
 #ifndef FEDMX_EXACT_ADAM
@@ -150,20 +160,24 @@ __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4
 }
 
 // LDS plan (floats); total < 160 KiB -> one workgroup per CU.
-constexpr int L_W1 = HP * S_W1;          // 4224  shared, column block per wave
+constexpr int L_W1 = HP * S_W1;          // 4224  master (snapshots / write-back only)
 constexpr int L_W4 = DP * S_W4;          // 4608  shared, row block per wave
 constexpr int L_W2 = ZP * S_W2;          // 576   shared master
 constexpr int L_W3 = HP * S_W3;          // 640   shared master
 constexpr int L_RED = 4 * 2 * 64 * 4;    // 2048  one partial-sum exchange buffer
 constexpr int L_T32 = 32 * S_T;          // 640   [32 features][batch] transpose tile
 constexpr int L_T16 = 16 * S_T;          // 320
-constexpr int L_SCR = 4 * L_T32 + 2 * L_T16;  // 3200 per wave
+constexpr int L_SCR = 3 * L_T32 + 2 * L_T16;  // 2560 per wave
 constexpr int L_TOTAL = L_W1 + L_W4 + L_W2 + L_W3 + 3 * L_RED + 4 * L_SCR + 64;
 
-// Per-lane state of the big owned blocks (MFMA D layouts):
-//   q1[t][v][r] = W1a[16t+4g+r][32w+16v+c]      q4[v][t][r] = W4a[32w+16v+4g+r][16t+c]
+// Per-lane state of the owned parameter blocks of wave w, lane (c = l & 15, g = l >> 4):
+//   q1[t][v][r] = W1a[16t+c][32w+16v+4g+r]   (MFMA A-operand layout of layer 1:
+//                 register s of tile (t,v) is the A value of k-step s, so the
+//                 forward consumes the registers directly, and dW1^T tiles come
+//                 out of the MFMA in exactly this layout)
+//   q4[v][t][r] = W4a[32w+16v+4g+r][16t+c]   (D layout: A operand of dH3 = W4a^T dY)
 // plus the owned small tile o[r]:
-//   w<2 : W3a[16w+4g+r][c]                      w>=2: W2a[4g+r][16(w-2)+c]
+//   w<2 : W3a[16w+4g+r][c]                   w>=2: W2a[4g+r][16(w-2)+c]
 struct Slab {
   float q1[2][2][4];
   float q4[2][2][4];
@@ -171,36 +185,51 @@ struct Slab {
 };
 
 struct Lane {
-  float* w1;   // sW1 + 4g*S_W1 + 32w + c       (D-layout element base)
-  float* w4;   // sW4 + (32w+4g)*S_W4 + c
+  float* w1;   // sW1 + c*S_W1 + 32w + 4g      (+ 16t*S_W1 + 16v; 4 consecutive r)
+  float* w4;   // sW4 + (32w+4g)*S_W4 + c      (+ (16v+r)*S_W4 + 16t)
   float* own;  // owned small tile base (stride own_stride per r)
   int own_stride;
 };
 
-__device__ __forceinline__ void slab_to_lds(const Slab& o, const Lane& L) {
+__device__ __forceinline__ void w1_to_lds(const Slab& o, const Lane& L) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+      lds_write4(L.w1 + 16 * t * S_W1 + 16 * v, f32x4{o.q1[t][v][0], o.q1[t][v][1], o.q1[t][v][2], o.q1[t][v][3]});
+}
+
+__device__ __forceinline__ void w4own_to_lds(const Slab& o, const Lane& L) {
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int v = 0; v < 2; ++v) {
-        L.w1[(16 * t + r) * S_W1 + 16 * v] = o.q1[t][v][r];
-        L.w4[(16 * v + r) * S_W4 + 16 * t] = o.q4[v][t][r];
-      }
+      for (int v = 0; v < 2; ++v) L.w4[(16 * v + r) * S_W4 + 16 * t] = o.q4[v][t][r];
 #pragma unroll
   for (int r = 0; r < 4; ++r) L.own[r * L.own_stride] = o.o[r];
+}
+
+__device__ __forceinline__ void slab_to_lds(const Slab& o, const Lane& L) {
+  w1_to_lds(o, L);
+  w4own_to_lds(o, L);
 }
 
 __device__ __forceinline__ void lds_to_slab(Slab& o, const Lane& L) {
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const f32x4 q = lds_read4(L.w1 + 16 * t * S_W1 + 16 * v);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o.q1[t][v][r] = q[r];
+    }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int v = 0; v < 2; ++v) {
-        o.q1[t][v][r] = L.w1[(16 * t + r) * S_W1 + 16 * v];
-        o.q4[v][t][r] = L.w4[(16 * v + r) * S_W4 + 16 * t];
-      }
+      for (int v = 0; v < 2; ++v) o.q4[v][t][r] = L.w4[(16 * v + r) * S_W4 + 16 * t];
 #pragma unroll
   for (int r = 0; r < 4; ++r) o.o[r] = L.own[r * L.own_stride];
 }
@@ -249,6 +278,15 @@ __device__ __forceinline__ void masters_to_global(float* __restrict__ dst, const
   }
 }
 
+// One batch column tile ("chunk") of up to 16 rows, in the two register
+// layouts the step needs:
+//   f0/f1: feature-major B operand  X[b=c][32w+4g+s] / X[b=c][32w+16+4g+s]
+//   b0/b1: batch-major A operand    X[b=4g+s][32w+c] / X[b=4g+s][32w+16+c]
+// Rows past the chunk are zero; the bias column (DP-1) is 1 on real rows.
+struct XChunk {
+  f32x4 f0, f1, b0, b1;
+};
+
 template <bool PROX>
 __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   __shared__ __attribute__((aligned(16))) float lds[L_TOTAL];
@@ -263,16 +301,15 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   float* const sRedH1 = sW3 + L_W3;               // two buffers (parity)
   float* const sRedDH3 = sRedH1 + 2 * L_RED;
   float* const scr = sRedDH3 + L_RED + w * L_SCR;
-  float* const sXT = scr;                // X^T own 32 columns      [32][S_T]
-  float* const sH1T = sXT + L_T32;       // H1^T                    [32][S_T]
+  float* const sH1T = scr;               // H1^T                    [32][S_T]
   float* const sT0 = sH1T + L_T32;       // dY^T own rows, then dH3^T
-  float* const sT1 = sT0 + L_T32;        // H3^T, then dH1^T
+  float* const sT1 = sT0 + L_T32;        // H3^T
   float* const sZT = sT1 + L_T32;        // Z^T (with bias row)     [16][S_T]
   float* const sDZT = sZT + L_T16;       // dZ^T                    [16][S_T]
   double* const sLoss = reinterpret_cast<double*>(sRedDH3 + L_RED + 4 * L_SCR);  // [4][4] doubles
 
   Lane L;
-  L.w1 = sW1 + 4 * g * S_W1 + 32 * w + c;
+  L.w1 = sW1 + c * S_W1 + 32 * w + 4 * g;
   L.w4 = sW4 + (32 * w + 4 * g) * S_W4 + c;
   if (w < 2) {
     L.own = sW3 + (16 * w + 4 * g) * S_W3 + c;
@@ -281,7 +318,6 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
     L.own = sW2 + 4 * g * S_W2 + 16 * (w - 2) + c;
     L.own_stride = S_W2;
   }
-  const float* const a1p = sW1 + c * S_W1 + 32 * w + 4 * g;   // + 16t*S_W1 + 16v
   const float* const a4p = sW4 + (32 * w + c) * S_W4 + 4 * g;  // + 16v*S_W4 + 16t
   const float* const a2p = sW2 + c * S_W2 + 4 * g;             // + 16t
   const float* const a3p = sW3 + c * S_W3 + 4 * g;             // + 16t*S_W3
@@ -318,7 +354,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   }
   global_to_masters(Pg, sW1, sW4, sW2, sW3);
   __syncthreads();
-  lds_to_slab(P, L);   // masters keep the live parameters from here on
+  lds_to_slab(P, L);   // W2/W3/W4 masters stay live; W1 lives in registers only
   STAMP(true, 29);
 
   const int B = A.batch;
@@ -330,7 +366,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   const int nvb = (n_va + B - 1) / B;
   int step = A.adam_step[cid];
   int parity = 0;
-  const bool bias_lane = (w == 3 && g == 3);  // holds X column DP-1 (= 32*3 + 16 + 4*3 + 3)
+  const bool bias_lane = (w == 3 && g == 3);  // feature-major: X column DP-1 (= 32*3 + 16 + 4*3 + 3)
+  const bool bias_col = (w == 3 && c == 15);  // batch-major:   X column DP-1 (= 32*3 + 16 + 15), tile 1
   const int xcol = 32 * w + 4 * g;
   const float lam = A.lambda;
   const float inv_d = 1.0f / (float)d_in;
@@ -341,43 +378,78 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
     fm0[r] = (xcol + r < d_in) ? 1.f : 0.f;
     fm1[r] = (xcol + 16 + r < d_in) ? 1.f : 0.f;
   }
-
   bool stamp_fwd = false;
   (void)stamp_fwd;
-  auto load_x = [&](const float* X, int row0, int bcur, f32x4& x0, f32x4& x1) {
-    const bool ok = c < bcur;
-    const float* src = X + (size_t)(row0 + c) * DP + xcol;
-    x0 = ok ? *reinterpret_cast<const f32x4*>(src) : zero4();
-    x1 = ok ? *reinterpret_cast<const f32x4*>(src + 16) : zero4();
-    if (bias_lane) x1[3] = 1.f;
+
+  // rows [row0, row0 + bc) of X, bc in 1..16.  Branch-free prefetch: rows
+  // past the chunk read row0 (always valid); the zeroing / bias column are
+  // applied by finalize_chunk when the chunk is consumed, so issuing the
+  // loads never waits for them.
+  auto load_chunk = [&](const float* X, int row0, int bc, XChunk& x) {
+    const float* src = X + (size_t)(row0 + (c < bc ? c : 0)) * DP + xcol;
+    x.f0 = *reinterpret_cast<const f32x4*>(src);
+    x.f1 = *reinterpret_cast<const f32x4*>(src + 16);
+    const float* bsrc = X + (size_t)row0 * DP + 32 * w + c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = (4 * g + r < bc) ? 4 * g + r : 0;
+      x.b0[r] = bsrc[(size_t)rr * DP];
+      x.b1[r] = bsrc[(size_t)rr * DP + 16];
+    }
+  };
+  auto finalize_chunk = [&](int bc, XChunk& x) {
+    const bool ok = c < bc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool okr = 4 * g + r < bc;
+      x.f0[r] = ok ? x.f0[r] : 0.f;
+      x.f1[r] = ok ? x.f1[r] : 0.f;
+      x.b0[r] = okr ? x.b0[r] : 0.f;
+      x.b1[r] = okr ? (bias_col ? 1.f : x.b1[r]) : 0.f;
+    }
+    if (bias_lane) x.f1[3] = 1.f;
+  };
+  auto load_chunk_f = [&](const float* X, int row0, int bc, XChunk& x) {  // validation: feature-major only
+    const bool ok = c < bc;
+    const float* src = X + (size_t)(row0 + (ok ? c : 0)) * DP + xcol;
+    const f32x4 f0 = *reinterpret_cast<const f32x4*>(src);
+    const f32x4 f1 = *reinterpret_cast<const f32x4*>(src + 16);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x.f0[r] = ok ? f0[r] : 0.f;
+      x.f1[r] = ok ? f1[r] : 0.f;
+    }
+    if (bias_lane) x.f1[3] = 1.f;
   };
 
-  // Forward of one batch (layer 1 K-split + LDS reduction; layers 2-3 redundant;
-  // layer 4 on own rows).  Adds this lane's loss share (MSE of its own 32
-  // features; shrink term on wave 0 / lane group 0) to `lacc`.
-  auto forward = [&](const f32x4& x0, const f32x4& x1, int bcur, f32x4 (&h1)[2], f32x4& z, f32x4& zb,
-                     f32x4 (&h3)[2], f32x4 (&y)[2], float& norm_c, double& lacc) {
+  // Layer-1 partial product over this wave's 32 input columns, straight from
+  // the owned registers (no LDS traffic for W1).
+  auto l1_partial = [&](const XChunk& x, f32x4& acc0, f32x4& acc1) {
+    acc0 = zero4();
+    acc1 = zero4();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc0 = mfma16(P.q1[0][0][j], x.f0[j], acc0);
+      acc1 = mfma16(P.q1[1][0][j], x.f0[j], acc1);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc0 = mfma16(P.q1[0][1][j], x.f1[j], acc0);
+      acc1 = mfma16(P.q1[1][1][j], x.f1[j], acc1);
+    }
+  };
+
+  // Rest of the forward of one chunk: layer-1 K reduction through LDS
+  // (barrier #1), layers 2-3 (redundant per wave), layer 4 on own rows.  Adds
+  // this lane's loss share (MSE of its own 32 features; shrink term on wave 0 /
+  // lane group 0), normalised by the whole batch's row count bt.
+  auto forward_rest = [&](const f32x4& acc0, const f32x4& acc1, const XChunk& x, int bc, float inv_bt,
+                          f32x4 (&h1)[2], f32x4& z, f32x4& zb, f32x4 (&h3)[2], f32x4 (&y)[2], float& norm_c,
+                          double& lacc) {
     float* red = sRedH1 + parity * L_RED;
     const bool sf = stamp_fwd;
-    {
-      f32x4 acc0 = zero4(), acc1 = zero4();
-      const f32x4 a00 = lds_read4(a1p);
-      const f32x4 a01 = lds_read4(a1p + 16);
-      const f32x4 a10 = lds_read4(a1p + 16 * S_W1);
-      const f32x4 a11 = lds_read4(a1p + 16 * S_W1 + 16);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc0 = mfma16(a00[j], x0[j], acc0);
-        acc1 = mfma16(a10[j], x0[j], acc1);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc0 = mfma16(a01[j], x1[j], acc0);
-        acc1 = mfma16(a11[j], x1[j], acc1);
-      }
-      lds_write4(red + (w * 2 + 0) * 256 + lane * 4, acc0);
-      lds_write4(red + (w * 2 + 1) * 256 + lane * 4, acc1);
-    }
+    lds_write4(red + (w * 2 + 0) * 256 + lane * 4, acc0);
+    lds_write4(red + (w * 2 + 1) * 256 + lane * 4, acc1);
     STAMP(sf, 1);
     __syncthreads();  // barrier #1
     STAMP(sf, 2);
@@ -451,19 +523,18 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
     float sq = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float d0 = (y[0][r] - x0[r]) * fm0[r];
-      const float d1 = (y[1][r] - x1[r]) * fm1[r];
+      const float d0 = (y[0][r] - x.f0[r]) * fm0[r];
+      const float d1 = (y[1][r] - x.f1[r]) * fm1[r];
       sq += d0 * d0 + d1 * d1;
     }
-    sq = (c < bcur) ? sq : 0.f;
+    sq = (c < bc) ? sq : 0.f;
     float nz = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) nz += (4 * g + r < latent) ? z[r] * z[r] : 0.f;
     nz = sum_lane_groups(nz);
     norm_c = __builtin_amdgcn_sqrtf(nz);
-    const float inv_b = 1.0f / (float)bcur;
-    float contrib = sq * (inv_b * inv_d);
-    if (w == 0 && g == 0 && c < bcur) contrib += lam * norm_c * inv_b;
+    float contrib = sq * (inv_bt * inv_d);
+    if (w == 0 && g == 0 && c < bc) contrib += lam * norm_c * inv_bt;
     lacc += (double)contrib;
   };
 
@@ -482,22 +553,54 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
 
   for (int ep = 0; ep < A.epochs; ++ep) {
     double acc_tr = 0.0;
-    f32x4 xa, xb, na, nbx;
-    if (nb > 0) load_x(Xtr, 0, min(B, n_tr), xa, xb);
-    for (int bi = 0; bi < nb; ++bi) {
-      const int row0 = bi * B;
-      const int bcur = min(B, n_tr - row0);
+    // The epoch is a sequence of chunks (batch bi, column tile ch).  The next
+    // chunk's rows are prefetched one chunk ahead, and its layer-1 partial is
+    // issued at the end of the current chunk (after the Adam update of W1 when
+    // the current chunk closes a batch), where it overlaps the remaining
+    // optimizer work.
+    int bi = 0, ch = 0;
+    XChunk cur, nxt;
+    f32x4 l1a = zero4(), l1b = zero4();
+    if (nb > 0) {
+      load_chunk(Xtr, 0, min(16, min(B, n_tr)), cur);
+      finalize_chunk(min(16, min(B, n_tr)), cur);
+      l1_partial(cur, l1a, l1b);
+    }
+    f32x4 G1[2][2], G4[2][2], Go;
+    while (bi < nb) {
+      const int row_b = bi * B;
+      const int bt = min(B, n_tr - row_b);
+      const int nch = (bt + 15) >> 4;
+      const int bc = min(16, bt - 16 * ch);
+      const bool last = (ch == nch - 1);
+      // next chunk position
+      const int bi_n = last ? bi + 1 : bi;
+      const int ch_n = last ? 0 : ch + 1;
+      const bool has_next = bi_n < nb;
+      const int row_n = bi_n * B + 16 * ch_n;
+      const int bc_n = has_next ? min(16, min(B, n_tr - bi_n * B) - 16 * ch_n) : 0;
+      const float inv_bt = 1.0f / (float)bt;
+      if (ch == 0) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int v = 0; v < 2; ++v) {
+            G1[t][v] = zero4();
+            G4[v][t] = zero4();
+          }
+        Go = zero4();
+      }
       f32x4 h1[2], z, zb, h3[2], y[2];
       float norm_c;
-      const bool stamp_on = (ep == 0 && bi == STAMP_STEP);
+      const bool stamp_on = (ep == 0 && bi == STAMP_STEP && ch == 0);
       STAMP(stamp_on, 0);
       stamp_fwd = FEDMX_STAMPS && stamp_on;
-      forward(xa, xb, bcur, h1, z, zb, h3, y, norm_c, acc_tr);
+      forward_rest(l1a, l1b, cur, bc, inv_bt, h1, z, zb, h3, y, norm_c, acc_tr);
       STAMP(stamp_on, 3);
-      if (bi + 1 < nb) load_x(Xtr, row0 + B, min(B, n_tr - row0 - B), na, nbx);  // prefetch
+      if (has_next) load_chunk(Xtr, row_n, bc_n, nxt);  // prefetch
 
       // current W2a / W3a (all tiles, D layout) for the backward-data products;
-      // owners only rewrite the masters after barrier #2.
+      // owners only rewrite the masters after the batch's last barrier #2.
       float q2[2][4], q3[2][4];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -507,21 +610,13 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
           q3[t][r] = d3p[(16 * t + r) * S_W3];
         }
 
-      ++step;
-      b1pow *= (double)A.beta1;
-      b2pow *= (double)A.beta2;
-      K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
-      K.bc2s = (float)sqrt(1.0 - b2pow);
-      K.inv_bc2s = 1.0f / K.bc2s;
-      float prox_acc = 0.f;  // sum (p - anchor)^2 of owned params (pre-update)
-
-      // ---- dY (masked) and the transposes feeding dW4
-      const float scale = (c < bcur) ? 2.0f / (float)(bcur * d_in) : 0.f;
+      // ---- dY (masked, feature-major) and the transposes feeding dW4
+      const float scale = (c < bc) ? 2.0f / (float)(bt * d_in) : 0.f;
       f32x4 dy[2];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        dy[0][r] = (y[0][r] - xa[r]) * (scale * fm0[r]);
-        dy[1][r] = (y[1][r] - xb[r]) * (scale * fm1[r]);
+        dy[0][r] = (y[0][r] - cur.f0[r]) * (scale * fm0[r]);
+        dy[1][r] = (y[1][r] - cur.f1[r]) * (scale * fm1[r]);
         sT0[tw + r * S_T] = dy[0][r];
         sT0[tw + (16 + r) * S_T] = dy[1][r];
         sT1[tw + r * S_T] = h3[0][r];
@@ -540,37 +635,30 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         lds_write4(redw, acc0);
         lds_write4(redw + 256, acc1);
       }
+      // ---- stage H1^T, Z^T (read after barrier #2: no wave-level ordering needed)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sH1T[tw + r * S_T] = h1[0][r];
+        sH1T[tw + (16 + r) * S_T] = h1[1][r];
+        sZT[tw + r * S_T] = zb[r];
+      }
       STAMP(stamp_on, 4);
       wave_sync();
-      // ---- dW4 (own rows) + fused Adam
+      // ---- dW4 (own rows) accumulated over the batch's chunks
       {
         const f32x4 a0 = lds_read4(sT0 + tr);
         const f32x4 a1 = lds_read4(sT0 + tr + 16 * S_T);
         const f32x4 b0 = lds_read4(sT1 + tr);
         const f32x4 b1 = lds_read4(sT1 + tr + 16 * S_T);
-        f32x4 g00 = zero4(), g01 = zero4(), g10 = zero4(), g11 = zero4();
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          g00 = mfma16(a0[s], b0[s], g00);
-          g01 = mfma16(a0[s], b1[s], g01);
-          g10 = mfma16(a1[s], b0[s], g10);
-          g11 = mfma16(a1[s], b1[s], g11);
+          G4[0][0] = mfma16(a0[s], b0[s], G4[0][0]);
+          G4[0][1] = mfma16(a0[s], b1[s], G4[0][1]);
+          G4[1][0] = mfma16(a1[s], b0[s], G4[1][0]);
+          G4[1][1] = mfma16(a1[s], b1[s], G4[1][1]);
         }
-adam4<PROX>(P.q4[0][0], M.q4[0][0], V.q4[0][0], AN.q4[0][0], g00, K, prox_acc);
-        adam4<PROX>(P.q4[0][1], M.q4[0][1], V.q4[0][1], AN.q4[0][1], g01, K, prox_acc);
-        adam4<PROX>(P.q4[1][0], M.q4[1][0], V.q4[1][0], AN.q4[1][0], g10, K, prox_acc);
-        adam4<PROX>(P.q4[1][1], M.q4[1][1], V.q4[1][1], AN.q4[1][1], g11, K, prox_acc);
       }
       STAMP(stamp_on, 5);
-      // ---- stage X^T, H1^T, Z^T for the remaining weight gradients
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        sXT[tw + r * S_T] = xa[r];
-        sXT[tw + (16 + r) * S_T] = xb[r];
-        sH1T[tw + r * S_T] = h1[0][r];
-        sH1T[tw + (16 + r) * S_T] = h1[1][r];
-        sZT[tw + r * S_T] = zb[r];
-      }
       STAMP(stamp_on, 6);
       __syncthreads();  // barrier #2: dH3 partials of all waves visible
       STAMP(stamp_on, 7);
@@ -588,39 +676,53 @@ adam4<PROX>(P.q4[0][0], M.q4[0][0], V.q4[0][0], AN.q4[0][0], g00, K, prox_acc);
         for (int r = 0; r < 4; ++r) {
           const int h = 16 * t + 4 * g + r;
           s[r] = (h < hidden && h3[t][r] > 0.f) ? s[r] : 0.f;
-          sT0[tw + (16 * t + r) * S_T] = s[r];  // dH3^T (dY^T reads done)
         }
         dh3[t] = s;
       }
-      // ---- dZ = W3a^T dH3 (pre-update W3, every wave)
+      if (w < 2) {  // dH3^T for the owned dW3 tile (dY^T reads are done)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sT0[tw + (16 * t + r) * S_T] = dh3[t][r];
+      }
+      // ---- dZ = W3a^T dH3 (pre-update W3, every wave), + shrink-loss gradient
+      //      lambda/B * z / ||z|| (0 where ||z|| == 0)
       f32x4 dz = zero4();
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int s = 0; s < 4; ++s) dz = mfma16(q3[t][s], dh3[t][s], dz);
-      // shrink-loss gradient: lambda/B * z / ||z|| (0 where ||z|| == 0)
-      const float shr = (c < bcur && norm_c > 0.f) ? lam / ((float)bcur * norm_c) : 0.f;
+      const float shr_raw = lam * __builtin_amdgcn_rcpf((float)bt * norm_c);
+      const float shr = (c < bc && norm_c > 0.f) ? shr_raw : 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        dz[r] = (4 * g + r < latent) ? dz[r] + shr * z[r] : 0.f;
-        sDZT[tw + r * S_T] = dz[r];
+      for (int r = 0; r < 4; ++r) dz[r] = (4 * g + r < latent) ? dz[r] + shr * z[r] : 0.f;
+      if (w >= 2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sDZT[tw + r * S_T] = dz[r];
       }
-      // ---- dH1 = W2a^T dZ (pre-update W2) -> dH1^T staged in sT1 (H3^T reads done)
-      {
-        f32x4 acc0 = zero4(), acc1 = zero4();
+      // ---- dH1 in the batch-major layout, D[b=4g+r][h=16t+c] = sum_z dZ[b][z] W2a[z][h]
+      //      (A = dZ^T D tile as is, B = W2a D layout), ReLU mask from H1^T
+      //      read in the same layout; this is directly dW1's B operand.
+      f32x4 dh1b[2], h1b[2];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          acc0 = mfma16(q2[0][s], dz[s], acc0);
-          acc1 = mfma16(q2[1][s], dz[s], acc1);
-        }
+      for (int t = 0; t < 2; ++t) {
+        h1b[t] = lds_read4(sH1T + tr + 16 * t * S_T);
+        f32x4 acc = zero4();
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int h0 = 4 * g + r, h1i = 16 + 4 * g + r;
-          sT1[tw + r * S_T] = (h0 < hidden && h1[0][r] > 0.f) ? acc0[r] : 0.f;
-          sT1[tw + (16 + r) * S_T] = (h1i < hidden && h1[1][r] > 0.f) ? acc1[r] : 0.f;
-        }
+        for (int s = 0; s < 4; ++s) acc = mfma16(dz[s], q2[t][s], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = (16 * t + c < hidden && h1b[t][r] > 0.f) ? acc[r] : 0.f;
+        dh1b[t] = acc;
       }
       STAMP(stamp_on, 8);
+      // ---- dW1^T (own columns) = X^T dH1: D[d=4g+r][h=c] lands in the q1 layout
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        G1[0][0] = mfma16(cur.b0[s], dh1b[0][s], G1[0][0]);
+        G1[0][1] = mfma16(cur.b1[s], dh1b[0][s], G1[0][1]);
+        G1[1][0] = mfma16(cur.b0[s], dh1b[1][s], G1[1][0]);
+        G1[1][1] = mfma16(cur.b1[s], dh1b[1][s], G1[1][1]);
+      }
       wave_sync();
       // ---- owned small tile: w<2 -> dW3 tile (h-block w) = dH3^T Z ;
       //                        w>=2 -> dW2 tile (h-block w-2) = dZ^T H1
@@ -631,56 +733,67 @@ adam4<PROX>(P.q4[0][0], M.q4[0][0], V.q4[0][0], AN.q4[0][0], g00, K, prox_acc);
           b = lds_read4(sZT + tr);
         } else {
           a = lds_read4(sDZT + tr);
-          b = lds_read4(sH1T + tr + 16 * (w - 2) * S_T);
+          b = (w == 2) ? h1b[0] : h1b[1];
         }
-        f32x4 acc = zero4();
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
-        adam4<PROX>(P.o, M.o, V.o, AN.o, acc, K, prox_acc);
+        for (int s = 0; s < 4; ++s) Go = mfma16(a[s], b[s], Go);
       }
       STAMP(stamp_on, 9);
-      // ---- dW1 (own columns) = dH1^T X + fused Adam
-      {
-        const f32x4 a0 = lds_read4(sT1 + tr);
-        const f32x4 a1 = lds_read4(sT1 + tr + 16 * S_T);
-        const f32x4 b0 = lds_read4(sXT + tr);
-        const f32x4 b1 = lds_read4(sXT + tr + 16 * S_T);
-        f32x4 g00 = zero4(), g01 = zero4(), g10 = zero4(), g11 = zero4();
+      if (last) {
+        ++step;
+        b1pow *= (double)A.beta1;
+        b2pow *= (double)A.beta2;
+        K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
+        K.bc2s = (float)sqrt(1.0 - b2pow);
+        K.inv_bc2s = 1.0f / K.bc2s;
+        float prox_acc = 0.f;  // sum (p - anchor)^2 of owned params (pre-update)
+        // W1 first: the next chunk's layer-1 product waits on it
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          g00 = mfma16(a0[s], b0[s], g00);
-          g01 = mfma16(a0[s], b1[s], g01);
-          g10 = mfma16(a1[s], b0[s], g10);
-          g11 = mfma16(a1[s], b1[s], g11);
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int v = 0; v < 2; ++v) adam4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
+        STAMP(stamp_on, 10);
+        if (has_next) {
+          finalize_chunk(bc_n, nxt);
+          l1_partial(nxt, l1a, l1b);
         }
-adam4<PROX>(P.q1[0][0], M.q1[0][0], V.q1[0][0], AN.q1[0][0], g00, K, prox_acc);
-        adam4<PROX>(P.q1[0][1], M.q1[0][1], V.q1[0][1], AN.q1[0][1], g01, K, prox_acc);
-        adam4<PROX>(P.q1[1][0], M.q1[1][0], V.q1[1][0], AN.q1[1][0], g10, K, prox_acc);
-        adam4<PROX>(P.q1[1][1], M.q1[1][1], V.q1[1][1], AN.q1[1][1], g11, K, prox_acc);
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) adam4<PROX>(P.q4[v][t], M.q4[v][t], V.q4[v][t], AN.q4[v][t], G4[v][t], K, prox_acc);
+        adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
+        if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
+        // publish own W4 rows (read back by this wave only) and the owned small tile
+        w4own_to_lds(P, L);
+      } else {
+        finalize_chunk(bc_n, nxt);
+        l1_partial(nxt, l1a, l1b);
       }
-      STAMP(stamp_on, 10);
-      if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
-      // publish the updated parameters (own W1 columns / W4 rows / small tile)
-      slab_to_lds(P, L);
-      wave_sync();
       STAMP(stamp_on, 11);
-      xa = na;
-      xb = nbx;
+      cur = nxt;
+      bi = bi_n;
+      ch = ch_n;
     }
 
     // ---- validation pass (eval mode, no grad)
     double acc_va = 0.0;
-    for (int bi = 0; bi < nvb; ++bi) {
-      const int row0 = bi * B;
-      const int bcur = min(B, n_va - row0);
-      f32x4 va, vb;
-      STAMP(ep == 0 && bi == 1, 16);
-      load_x(Xva, row0, bcur, va, vb);
-      f32x4 h1[2], z, zb, h3[2], y[2];
-      float norm_c;
-      STAMP(ep == 0 && bi == 1, 17);
-      forward(va, vb, bcur, h1, z, zb, h3, y, norm_c, acc_va);
-      STAMP(ep == 0 && bi == 1, 18);
+    for (int vb = 0; vb < nvb; ++vb) {
+      const int row0 = vb * B;
+      const int bt = min(B, n_va - row0);
+      const float inv_bt = 1.0f / (float)bt;
+      for (int c0 = 0; c0 < bt; c0 += 16) {
+        const int bc = min(16, bt - c0);
+        XChunk xv;
+        STAMP(ep == 0 && vb == 1 && c0 == 0, 16);
+        load_chunk_f(Xva, row0 + c0, bc, xv);
+        f32x4 a0, a1;
+        l1_partial(xv, a0, a1);
+        f32x4 h1[2], z, zb, h3[2], y[2];
+        float norm_c;
+        STAMP(ep == 0 && vb == 1 && c0 == 0, 17);
+        forward_rest(a0, a1, xv, bc, inv_bt, h1, z, zb, h3, y, norm_c, acc_va);
+        STAMP(ep == 0 && vb == 1 && c0 == 0, 18);
+      }
     }
     STAMP(ep == 0, 12);
     double prox_now = 0.0;
@@ -703,6 +816,8 @@ adam4<PROX>(P.q1[0][0], M.q1[0][0], V.q1[0][0], AN.q1[0][0], g00, K, prox_acc);
       }
       prox_now = (double)pr;
     }
+    // W1 master for a possible best-validation snapshot (covered by the barrier below)
+    w1_to_lds(P, L);
     // ---- epoch-end reduction (fixed order over waves -> identical decision everywhere)
     {
       const double s0 = wave_sum_d(acc_tr);
@@ -742,6 +857,8 @@ adam4<PROX>(P.q1[0][0], M.q1[0][0], V.q1[0][0], AN.q1[0][0], g00, K, prox_acc);
 
   STAMP(true, 30);
   // ---- write back: params (masters), then m and v through the same staging
+  w1_to_lds(P, L);
+  __syncthreads();
   masters_to_global(Pg, sW1, sW4, sW2, sW3);
   __syncthreads();
   slab_to_lds(M, L);
@@ -766,7 +883,7 @@ extern "C" {
 int fedmx_train(const void* args, int k, hipStream_t stream) {
   if (k <= 0) return 0;
   const fedmx::TrainArgs& A = *reinterpret_cast<const fedmx::TrainArgs*>(args);
-  if (A.batch < 1 || A.batch > 16) return -2;
+  if (A.batch < 1) return -2;
   if (A.d_in < 1 || A.d_in > fedmx::DP - 1 || A.hidden < 1 || A.hidden > fedmx::HP - 1 || A.latent < 1 ||
       A.latent > fedmx::ZP - 1)
     return -3;

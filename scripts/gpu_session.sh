@@ -45,4 +45,10 @@ if [ "$MODE" = pmc ]; then
   step pmc 300 rocprofv3 --kernel-trace --stats --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d "$OUT/pmc" -o pmc -- python3 "$ROOT/scripts/bench_kernels.py" --reps 3
   cd "$ROOT"
 fi
+if [ "$MODE" = pmctrain ]; then
+  cd /tmp && export TMPDIR=/tmp
+  step pmc_train1 300 rocprofv3 --kernel-trace --stats --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA -d "$OUT/pmc_train1" -o pmc -- python3 "$ROOT/scripts/train_stamps.py" --plain
+  step pmc_train2 300 rocprofv3 --kernel-trace --stats --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC -d "$OUT/pmc_train2" -o pmc -- python3 "$ROOT/scripts/train_stamps.py" --plain
+  cd "$ROOT"
+fi
 echo "=== done"

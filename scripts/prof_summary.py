@@ -61,12 +61,28 @@ def main(argv=None):
     ap.add_argument("db")
     ap.add_argument("--title", default="rocprofv3 kernel summary")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--pmc", action="store_true", help="the database holds PMC counters")
+    ap.add_argument("--kernel", default="", help="only kernels whose name contains this")
     a = ap.parse_args(argv)
-    text = summarize(a.db, a.title)
+    text = (f"# {a.title}\n\nsource: `{a.db}`\n\n" + pmc_summary(a.db, a.kernel)) if a.pmc else summarize(a.db, a.title)
     if a.out:
         with open(a.out, "w") as f:
             f.write(text)
     sys.stdout.write(text)
+
+
+def pmc_summary(db: str, kernel_substr: str = "") -> str:
+    """Per-kernel PMC counter totals (and per-dispatch means) from a --pmc run."""
+    c = sqlite3.connect(db)
+    rows = c.execute("select k.name, p.counter_name, sum(p.counter_value), count(distinct k.id) "
+                     "from pmc_events p join kernels k on p.event_id = k.id "
+                     "group by k.name, p.counter_name").fetchall()
+    out = ["| kernel | counter | total | per dispatch |", "|---|---|---|---|"]
+    for name, cn, v, n in sorted(rows):
+        if kernel_substr and kernel_substr not in name:
+            continue
+        out.append(f"| `{_short(name, 40)}` | {cn} | {v:.0f} | {v / max(n, 1):.0f} |")
+    return "\n".join(out) + "\n"
 
 
 if __name__ == "__main__":

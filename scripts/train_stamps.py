@@ -13,7 +13,9 @@ import sys
 
 ROOT = __file__.rsplit("/scripts/", 1)[0]
 sys.path.insert(0, ROOT)
-os.environ["FEDMX_HIP_LIB"] = os.path.join(ROOT, "fedmse_decentralized_amd/ops/lib/libfedmx_hip_stamps.so")
+PLAIN = "--plain" in sys.argv   # regular build, no stamps (for PMC counter runs)
+if not PLAIN:
+    os.environ["FEDMX_HIP_LIB"] = os.path.join(ROOT, "fedmse_decentralized_amd/ops/lib/libfedmx_hip_stamps.so")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -27,17 +29,18 @@ from fedmse_decentralized_amd.models.reference import init_client_params  # noqa
 from fedmse_decentralized_amd.ops import _hip, build  # noqa: E402
 
 PHASES = [
-    (0, 1, "fwd L1 mfma + partial write"), (1, 2, "barrier #1"), (2, 3, "fwd reduce + L2..L4 + loss"),
-    (3, 4, "dY/transposes + dH3 partial"), (4, 5, "dW4 mfma + adam"), (5, 6, "stage X/H1/Z"),
-    (6, 7, "barrier #2"), (7, 8, "dH3 reduce + dZ + dH1"), (8, 9, "small tile mfma + adam"),
-    (9, 10, "dW1 mfma + adam"), (10, 11, "publish + wave_sync"), (0, 11, "TRAIN STEP TOTAL"),
-    (16, 17, "valid: load_x"), (17, 18, "valid: forward"), (28, 29, "prologue (state load)"),
+    (0, 1, "L1 partial write"), (1, 2, "barrier #1"), (2, 3, "fwd reduce + L2..L4 + loss"),
+    (3, 4, "prefetch + dY/transposes + dH3 partial + stage"), (4, 5, "dW4 mfma"),
+    (6, 7, "barrier #2"), (7, 8, "dH3 reduce + dZ + dH1 (batch-major)"), (8, 9, "dW1 mfma + small tile"),
+    (9, 10, "adam W1"), (10, 11, "next L1 + adam W4/small + publish"), (0, 11, "TRAIN STEP TOTAL"),
+    (16, 17, "valid: load chunk + L1"), (17, 18, "valid: forward rest"), (28, 29, "prologue (state load)"),
     (12, 13, "epoch end (reduce + snapshot)"), (30, 31, "epilogue (write back)"),
 ]
 
 
 def main():
-    build.build_hip(extra_flags=["-DFEDMX_STAMPS=1"], target=build.HIP_STAMPS_LIB)
+    if not PLAIN:
+        build.build_hip(extra_flags=["-DFEDMX_STAMPS=1"], target=build.HIP_STAMPS_LIB)
     dev = torch.device("cuda", 0)
     raws = generate_federation(SyntheticSpec(kind="nbaiot", n_clients=10, seed=1))
     clients, _ = prepare_federation(raws, 1234)
@@ -47,6 +50,12 @@ def main():
               [c.test_label for c in clients], init)
     hp = TrainHParams(epochs=5, batch_size=12, lr=1e-3, shrink_lambda=5.0, patience=10 ** 6)
     stamps = torch.zeros(4 * 32, dtype=torch.int64, device=dev)
+    if PLAIN:
+        for _ in range(3):
+            _hip.train(eng.store, list(range(5)), hp, eng.dims)
+        torch.cuda.synchronize()
+        print("plain train launches done")
+        return
     out = {}
     for rep in range(3):
         _hip.train(eng.store, list(range(5)), hp, eng.dims, stamps=stamps)

@@ -116,7 +116,7 @@ def _setup_pair(n_train=(53, 40), n_valid=(14, 9), seed=0):
 
 
 @pytest.mark.parametrize("lam,mu,batch", [(5.0, 0.0, 12), (0.0, 0.0, 12), (5.0, 0.001, 12), (10.0, 0.0, 16),
-                                          (1.0, 0.01, 7)])
+                                          (1.0, 0.01, 7), (5.0, 0.0, 33), (5.0, 0.001, 64), (5.0, 0.0, 128)])
 def test_train_kernel_matches_torch_engine(lam, mu, batch):
     ref, hip = _setup_pair()
     # non-trivial FedProx anchor
