@@ -72,6 +72,31 @@ class ExperimentConfig:
     log_level: str = "INFO"
     malicious_clients: List[int] = field(default_factory=list)  # fault injection (tests)
     malicious_scale: float = 10.0
+    dropped_clients: List[int] = field(default_factory=list)    # fault injection: never vote / aggregate
+    # --- protocol variants ---------------------------------------------------
+    # "first_voter": the reference's decentralised election (first selected
+    #   voter that finds an eligible candidate decides, client_trainer.py:249-285);
+    # "majority": the legacy centralised GlobalAggregator.select_aggregator
+    #   (every selected client votes, most votes wins).
+    election: str = "first_voter"
+    # "decentralized": receivers verify the broadcast aggregate (reference);
+    # "centralized": server push, every client adopts the aggregate (legacy
+    #   GlobalAggregator.update).
+    aggregation_mode: str = "decentralized"
+    # "code": ModelVerifier rule (drift <= 3.0 and dperf >= -0.002);
+    # "thesis": the thesis variant (Thesis p.20-26): loss-ratio acceptance
+    #   new <= old * (1 + thesis_loss_ratio) with a NaN/inf check, candidates
+    #   with vote MSE > thesis_vote_mse_cap are not voted for, and a random
+    #   eligible aggregator is used when no valid one exists.
+    protocol_variant: str = "code"
+    thesis_loss_ratio: float = 0.1
+    thesis_vote_mse_cap: float = 3.0
+    fusion_max_rows: int = 1024          # dev rows used by the fusion_avg KDE similarity
+    # experiment-level parallelism: with N ranks, combination
+    # i of the model_type x update_type x run sweep runs on rank i % N (each
+    # as a single-rank federation on that rank's GPU) instead of every
+    # combination being sharded over all ranks.
+    parallel_combos: bool = False
 
     # -----------------------------------------------------------------------
     @property

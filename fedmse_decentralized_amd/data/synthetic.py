@@ -206,3 +206,32 @@ def generate_federation(spec: SyntheticSpec, clients: Optional[List[int]] = None
     s = spec.resolved()
     ids = range(s.n_clients) if clients is None else clients
     return [generate_client(s, c) for c in ids]
+
+
+def write_dataset(out_dir: str, spec: SyntheticSpec, config_name: Optional[str] = None) -> str:
+    """Materialise a synthetic federation on disk in the reference's layout —
+    headerless 115-column CSVs under ``Client-k/{normal,abnormal,test_normal}/data.csv``
+    plus a device-list JSON with the schema of `src/Configuration/*.json`
+     — so the CSV ingest path (``--config-file``) runs end to end
+    without the reference's data.  Returns the JSON path."""
+    import json
+    import os
+
+    data_dir = os.path.join(out_dir, "Data")
+    cfg_dir = os.path.join(out_dir, "Configuration")
+    os.makedirs(cfg_dir, exist_ok=True)
+    devices = []
+    for i, raw in enumerate(generate_federation(spec)):
+        base = f"Client-{i + 1}"
+        for split, arr in (("normal", raw.normal), ("abnormal", raw.abnormal), ("test_normal", raw.test_normal)):
+            d = os.path.join(data_dir, base, split)
+            os.makedirs(d, exist_ok=True)
+            np.savetxt(os.path.join(d, "data.csv"), arr, delimiter=",", fmt="%.10g")
+        devices.append({"id": i + 1, "name": raw.name, "normal_data_path": f"{base}/normal",
+                        "abnormal_data_path": f"{base}/abnormal", "test_normal_data_path": f"{base}/test_normal"})
+    name = config_name or f"synthetic-{spec.kind}-{spec.n_clients}clients.json"
+    path = os.path.join(cfg_dir, name)
+    # data_path is relative to the directory the driver resolves from (the JSON's parent's parent)
+    with open(path, "w") as f:
+        json.dump({"data_path": "Data", "devices_list": devices}, f, indent=4)
+    return path

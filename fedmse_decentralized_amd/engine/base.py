@@ -233,6 +233,15 @@ class Engine:
         drift = self.param_drift(hist, agg) if hist is not None and hist.shape[0] else torch.zeros(0)
         return mse, drift
 
+    def model_mse(self, local_rows: Sequence[int], datasets: Sequence[torch.Tensor]) -> np.ndarray:
+        """float64 [k]: MSE of each local row's own current model on its dataset
+        (thesis verification's old loss)."""
+        if not len(local_rows):
+            return np.zeros(0)
+        sse, _ = self.forward_rows(self.store.params, list(zip(local_rows, datasets)), want_sse=True)
+        D = self.dims.d_in
+        return np.array([batch_mean_scores(s, 1 << 30, D)[1] for s in sse], dtype=np.float64)
+
     def adopt(self, local_rows: Sequence[int], agg: torch.Tensor, anchor: bool = True) -> None:
         st = self.store
         if not len(local_rows):

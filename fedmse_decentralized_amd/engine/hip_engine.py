@@ -136,6 +136,13 @@ class HipEngine(Engine):
             drift = np.zeros(0, dtype=np.float32)
         return mse, drift
 
+    def model_mse(self, local_rows, datasets):
+        if not len(local_rows):
+            return np.zeros(0)
+        sse, _ = _hip.forward_rows(self.store.params, list(zip(local_rows, datasets)), self.dims, True, False)
+        red = _hip.score_reduce(sse, [0] * len(sse), self.dims.d_in)
+        return self.fetch([_ColView(red, 1)])[0]
+
     def adopt(self, local_rows, agg, anchor=True):
         st = self.store
         _hip.broadcast_rows(st.params, st.anchor if anchor else None, list(local_rows), agg)

@@ -43,8 +43,8 @@ from .parallel.comm import Comm, LoopbackComm
 from .parallel.sharding import ShardMap
 from .protocol.aggregation import make_plan
 from .protocol.early_stop import GlobalEarlyStop
-from .protocol.election import elect_aggregator, select_clients
-from .protocol.verification import Verifier, VerifierState
+from .protocol.election import elect_aggregator, elect_majority, select_clients
+from .protocol.verification import ThesisVerifier, Verifier, VerifierState
 from .utils.rng_replay import HostNoise, TorchRngReplay
 from .utils.telemetry import Telemetry
 
@@ -158,8 +158,15 @@ class Federation:
         self.valid_all = [eng.to_device(c.valid) for c in clients]
         self.dev_set = eng.to_device(dev)
         self.agg_counts = [0] * N
-        self.verifier = Verifier(cfg.verification_threshold, cfg.performance_threshold,
-                                 cfg.verification_method, cfg.max_rejected_updates)
+        if cfg.protocol_variant == "thesis":
+            self.verifier = ThesisVerifier(cfg.thesis_loss_ratio, cfg.verification_method, cfg.max_rejected_updates)
+        else:
+            self.verifier = Verifier(cfg.verification_threshold, cfg.performance_threshold,
+                                     cfg.verification_method, cfg.max_rejected_updates)
+        # thesis variant: random aggregator fallback (own stream: the reference RNG order is untouched)
+        self.fallback_rng = random.Random(cfg.data_seed + 7919 * (self.run + 1)) \
+            if cfg.protocol_variant == "thesis" else None
+        self._dev_kde = None
         self.vstate: Dict[int, VerifierState] = {c: VerifierState() for c in self.local}
         self.versions: Dict[int, torch.Tensor] = {}
         self.last_received: List[Optional[int]] = [None] * N
@@ -249,6 +256,8 @@ class Federation:
 
         with self.tel.phase("select"):
             selected = select_clients(self.py_rng, N, cfg.num_participants)
+            if cfg.dropped_clients:   # fault injection: offline clients neither train, vote nor aggregate
+                selected = [c for c in selected if c not in cfg.dropped_clients]
             local_sel = [c for c in selected if self._mine(c)]
             local_rows = [self._loc(c) for c in local_sel]
 
@@ -266,7 +275,8 @@ class Federation:
         # ---------------- vote scores (+ FedMSE dev MSE) of the local selected clients
         with self.tel.phase("vote"):
             need_dev = self.update_type == "mse_avg"
-            scores_dev = eng.vote_scores(local_rows, self.valid_all[selected[0]],
+            vote_data = self.valid_all[selected[0]] if selected else self.dev_set
+            scores_dev = eng.vote_scores(local_rows, vote_data,
                                          self.dev_set if need_dev else None, cfg.vote_batch_size)
             # first host sync of the round: training results + scores
             host = eng.fetch((handle.tensors if handle is not None else []) + [scores_dev])
@@ -298,8 +308,10 @@ class Federation:
             epochs_all = {c: int(vec[c, 2]) for c in selected}
             # torch-RNG replay (compat): one iterator per train and per valid epoch loop
             self.noise.iterators(2 * sum(epochs_all.values()))
-            el = elect_aggregator(selected, base_scores, self.agg_counts, cfg.max_aggregation, self.noise,
-                                  log_enabled=info)
+            elect = elect_majority if cfg.election == "majority" else elect_aggregator
+            cap = cfg.thesis_vote_mse_cap if cfg.protocol_variant == "thesis" else None
+            el = elect(selected, base_scores, self.agg_counts, cfg.max_aggregation, self.noise,
+                       log_enabled=info, vote_mse_cap=cap, fallback_rng=self.fallback_rng)
             aggregator = el.aggregator
 
         verification_results: List[Dict] = []
@@ -310,7 +322,10 @@ class Federation:
                 if self.update_type == "mse_avg":
                     for _ in selected:          # calculate_mse_score per client (weights unused, Q3)
                         self.noise.rand()
-                plan = make_plan(self.update_type, selected, aggregator, dev_mse, cfg.compat)
+                sim = None
+                if self.update_type == "fusion_avg":
+                    sim = self._fusion_similarity(selected)
+                plan = make_plan(self.update_type, selected, aggregator, dev_mse, cfg.compat, sim=sim)
             with self.tel.phase("comm"):
                 stack = self._gather_params([c for c, _ in plan], selected)
             with self.tel.phase("aggregate"):
@@ -320,9 +335,19 @@ class Federation:
                     eng.adopt([self._loc(aggregator)], agg, anchor=False)
                 version = rnd
                 self.versions[version] = agg
-            with self.tel.phase("verify"):
-                verification_results = self._verify_all(agg, version, aggregator, rnd)
-            if self.write_reports:
+            if cfg.aggregation_mode == "centralized":
+                # server push (legacy GlobalAggregator.update): every hosted client
+                # loads the aggregate and re-anchors FedProx; nothing is verified
+                with self.tel.phase("aggregate"):
+                    others = [self._loc(c) for c in self.local if c != aggregator]
+                    eng.adopt(others, agg, anchor=True)
+                    if self._mine(aggregator):
+                        eng.adopt([self._loc(aggregator)], agg, anchor=True)
+                    self.versions.pop(version, None)
+            else:
+                with self.tel.phase("verify"):
+                    verification_results = self._verify_all(agg, version, aggregator, rnd)
+            if self.write_reports and cfg.aggregation_mode != "centralized":
                 if info:
                     log.info("Verification results for this round:")
                     for r_ in verification_results:
@@ -382,16 +407,27 @@ class Federation:
         keys = sorted(set(key_of.values()))
         need = sorted({self.vstate[c].history_version for c in receivers if self.vstate[c].history_version is not None})
         hist = torch.stack([self.versions[v] for v in need], 0) if need else None
+        thesis = isinstance(self.verifier, ThesisVerifier)
+        if thesis:
+            hist = None
         mse_t, drift_t = eng.verify_stats(agg, [data_of[k] for k in keys], hist)
         mse_np, drift_np = eng.fetch([mse_t, drift_t])
         perf = {k: 1.0 / (1.0 + float(m)) for k, m in zip(keys, mse_np)}   # 1 / (1 + MSE)
+        new_loss = {k: float(m) for k, m in zip(keys, mse_np)}
+        old_loss = {}
+        if thesis and receivers:   # each receiver's own current model on the same data
+            own = eng.model_mse([self._loc(c) for c in receivers], [data_of[key_of[c]] for c in receivers])
+            old_loss = {c: float(x) for c, x in zip(receivers, own)}
         drift = {v: float(x) for v, x in zip(need, drift_np)}
         accept = []
         vec = np.zeros((N, 2), dtype=np.float64)
         for c in receivers:
             vs_ = self.vstate[c]
-            dr = drift.get(vs_.history_version, 0.0) if vs_.history_version is not None else 0.0
-            dec = self.verifier.decide(c, vs_, version, perf[key_of[c]], dr, rnd)
+            if thesis:
+                dec = self.verifier.decide_losses(c, vs_, version, old_loss[c], new_loss[key_of[c]], rnd)
+            else:
+                dr = drift.get(vs_.history_version, 0.0) if vs_.history_version is not None else 0.0
+                dec = self.verifier.decide(c, vs_, version, perf[key_of[c]], dr, rnd)
             self.verifier.apply(c, vs_, dec)
             if dec.verified:
                 accept.append(c)
@@ -417,6 +453,39 @@ class Federation:
             rej = int(vec[c, 0])
             out.append({"client_id": c, "rejected_updates": rej, "is_verified": rej == 0})
         return out
+
+    def _fusion_similarity(self, selected: Sequence[int]) -> Dict[int, float]:
+        """fusion_avg: JS distance between the KDE density of the dev set and
+        that of each selected model's reconstruction of it (host, subsampled
+        to ``fusion_max_rows`` dev rows; identical on every rank)."""
+        return self._fusion_similarity_of(self._gather_params(list(selected), selected), selected)
+
+    def _fusion_similarity_of(self, stack: torch.Tensor, ids: Sequence[int]) -> Dict[int, float]:
+        from .models.layout import padded_to_canonical
+        from .models.reference import functional_forward, unflatten
+        from .utils.similarity import kde_log_density, similarity_score
+
+        D = self.dims.d_in
+        dev = self.dev_set[: self.cfg.fusion_max_rows, :D].detach().float().cpu()
+        if self._dev_kde is None:
+            self._dev_kde = kde_log_density(dev.numpy())
+        stack = stack.detach().float().cpu()
+        out = {}
+        with torch.no_grad():
+            for i, c in enumerate(ids):
+                t = unflatten(padded_to_canonical(stack[i], self.dims), self.dims)
+                _, y = functional_forward(t, dev)
+                out[c] = similarity_score(self._dev_kde, y.numpy())
+        return out
+
+    # -- per-client peer API (reference ClientTrainer surface) ----------------------
+    def peer(self, cid: int):
+        from .protocol.peer import Peer
+
+        return Peer(self, cid)
+
+    def peers(self):
+        return [self.peer(c) for c in self.local]
 
     # -- whole combination -------------------------------------------------------
     def run_all(self) -> float:

@@ -9,6 +9,9 @@ executes ``sum_k w_k * theta_src(k)`` in plan order on the device
   `:132-134`; FedProx's proximal term lives in local training).
 * ``mse_avg`` (FedMSE) — weights proportional to ``1 / MSE`` of each model on
   the shared dev set (`src/Trainer/client_trainer.py:115-130`).
+* ``fusion_avg`` — the legacy centralised aggregator's KDE/JS-similarity
+  weighting: weights from ``utils.similarity.fusion_weights``
+  of each model's dev-set reconstruction similarity, computed by the caller.
 
 ``compat="reference"`` reproduces the state-dict aliasing of the reference's
 ``fed_mse_avg``: the aggregator loads every gathered state into
@@ -54,10 +57,22 @@ def plan_mse_avg(selected: Sequence[int], aggregator: int, dev_mse: Dict[int, fl
     return [(cid, w / tot) for cid, w in raw]
 
 
+def plan_fusion(selected: Sequence[int], sim: Dict[int, float]) -> Plan:
+    from ..utils.similarity import fusion_weights
+
+    w = fusion_weights([sim[c] for c in selected])
+    return [(cid, float(x)) for cid, x in zip(selected, w)]
+
+
+UPDATE_TYPES = ("avg", "fedprox", "mse_avg", "fusion_avg")
+
+
 def make_plan(update_type: str, selected: Sequence[int], aggregator: int, dev_mse: Dict[int, float] = None,
-              compat: str = "reference") -> Plan:
+              compat: str = "reference", sim: Dict[int, float] = None) -> Plan:
     if update_type in ("avg", "fedprox"):
         return plan_mean(selected)
     if update_type == "mse_avg":
         return plan_mse_avg(selected, aggregator, dev_mse, compat)
+    if update_type == "fusion_avg":
+        return plan_fusion(selected, sim)
     raise ValueError(f"Unknown update type: {update_type}")

@@ -74,3 +74,28 @@ class Verifier:
             log.warning("[Client %d] Model update rejected. Performance change: %.10f", client_id, dec.perf_change)
             if st.rejected_updates >= self.max_rejected:
                 log.error(f"[Client {client_id}] Too many rejected updates. Possible attack detected.")
+
+
+class ThesisVerifier(Verifier):
+    """The thesis's acceptance rule (Thesis p.20-22 Alg. 4.3, p.26 §4.3.6;
+    SURVEY §5.3): accept iff the aggregate's validation loss is finite and
+    ``new_loss <= old_loss * (1 + ratio)`` where ``old_loss`` is the
+    receiver's own current model on the same data; on reject the receiver
+    keeps (restores) its own model.  Rejection counting is unchanged."""
+
+    def __init__(self, ratio: float = 0.1, method: str = "val", max_rejected: int = 3):
+        super().__init__(method=method, max_rejected=max_rejected)
+        self.ratio = ratio
+
+    def needs_drift(self, st: VerifierState) -> bool:
+        return False
+
+    def decide_losses(self, client_id: int, st: VerifierState, version: int, old_loss: float, new_loss: float,
+                      current_round: int) -> VerifyDecision:
+        import math
+
+        st.history_version, st.history_perf, st.history_round = version, 1.0 / (1.0 + new_loss), current_round
+        ok = math.isfinite(new_loss) and new_loss <= old_loss * (1.0 + self.ratio)
+        if log.isEnabledFor(logging.INFO):
+            log.info(f"Client {client_id} - old loss: {old_loss:.10f}, new loss: {new_loss:.10f}")
+        return VerifyDecision(ok, old_loss - new_loss, 0.0)

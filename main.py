@@ -23,6 +23,7 @@ import torch
 from fedmse_decentralized_amd.config import ExperimentConfig, add_arguments, from_args
 from fedmse_decentralized_amd.federation import Federation
 from fedmse_decentralized_amd.io import reports
+from fedmse_decentralized_amd.parallel.comm import LoopbackComm
 from fedmse_decentralized_amd.parallel.launch import init_comm, shutdown
 from fedmse_decentralized_amd.protocol.early_stop import GlobalEarlyStop
 from fedmse_decentralized_amd.utils.logging import setup_logging
@@ -57,20 +58,27 @@ def run_sweep(cfg: ExperimentConfig, comm=None) -> dict:
     log.info(f"Backend: {cfg.backend}  compat: {cfg.compat}  world size: {comm.world_size}")
     log.info("=" * 50 + "\n")
     early = GlobalEarlyStop(cfg.global_patience, cfg.compat)   # process-global in compat mode (Q8)
-    k = 0
-    for model_type in cfg.model_types:
-        for update_type in cfg.update_types:
-            for run in range(cfg.num_runs):
-                k += 1
-                log.info(f"\nStarting combination {k}/{total}")
-                log.info(f"Model type: {model_type}, Update type: {update_type}, Run: {run + 1}/{cfg.num_runs}")
-                early.start_combination()
-                fed = Federation(cfg, model_type, update_type, run, comm=comm, early_stop=early).setup()
-                m = fed.run_all()
-                best[model_type][update_type] = max(best[model_type][update_type], m)
-                del fed
-                if torch.cuda.is_available():
-                    torch.cuda.empty_cache()
+    combos = [(mt, ut, run) for mt in cfg.model_types for ut in cfg.update_types for run in range(cfg.num_runs)]
+    parallel = cfg.parallel_combos and comm.world_size > 1
+    results = []
+    for k, (model_type, update_type, run) in enumerate(combos, start=1):
+        if parallel and (k - 1) % comm.world_size != comm.rank:
+            continue
+        log.info(f"\nStarting combination {k}/{total}")
+        log.info(f"Model type: {model_type}, Update type: {update_type}, Run: {run + 1}/{cfg.num_runs}")
+        early.start_combination()
+        # parallel combos: a single-rank federation on this rank's device
+        fcomm = LoopbackComm(comm.device) if parallel else comm
+        fed = Federation(cfg, model_type, update_type, run, comm=fcomm, early_stop=early).setup()
+        m = fed.run_all()
+        results.append((model_type, update_type, m))
+        del fed
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+    if parallel:
+        results = [r for part in comm.all_gather_object(results) for r in part]
+    for model_type, update_type, m in results:
+        best[model_type][update_type] = max(best[model_type][update_type], m)
     log.info("\nTraining Summary:")
     log.info("=" * 50)
     for mt in cfg.model_types:

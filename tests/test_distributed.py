@@ -79,3 +79,50 @@ def test_gloo_two_ranks_match_single_process(tmp_path):
             np.testing.assert_array_equal(np.array(a), b.metrics)
         loc = d["local"]
         assert d["params"] == ref_params[loc[0]:loc[-1] + 1]
+
+
+def _combo_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    _shrink()
+    import dataclasses
+
+    from fedmse_decentralized_amd.parallel.launch import init_comm, shutdown
+
+    sys_path = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import sys
+    sys.path.insert(0, sys_path)
+    import main as driver
+
+    comm = init_comm(backend="gloo", device="cpu")
+    cfg = dataclasses.replace(_cfg(out), parallel_combos=True, update_types=["avg", "fedprox", "mse_avg"],
+                              model_types=["hybrid"], num_rounds=1)
+    best = driver.run_sweep(cfg, comm=comm)
+    with open(os.path.join(out, f"combo_rank{rank}.json"), "w") as f:
+        json.dump(best, f)
+    shutdown(comm)
+
+
+@pytest.mark.timeout(300)
+def test_parallel_combos_two_ranks(tmp_path):
+    """Experiment-level parallelism: the 3 combinations split over 2 ranks give
+    the same summary as running them one after another in one process."""
+    out = str(tmp_path)
+    mp.start_processes(_combo_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    _shrink()
+    import dataclasses
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import main as driver
+    from fedmse_decentralized_amd import federation
+
+    federation._PREP_CACHE.clear()
+    cfg = dataclasses.replace(_cfg(out + "/seq"), update_types=["avg", "fedprox", "mse_avg"], model_types=["hybrid"],
+                              num_rounds=1)
+    ref = driver.run_sweep(cfg)
+    for r in range(2):
+        got = json.load(open(os.path.join(out, f"combo_rank{r}.json")))
+        assert got == ref
+    assert os.path.exists(os.path.join(out, "Checkpoint", "Results", "Update", "4"))

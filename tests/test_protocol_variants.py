@@ -1,0 +1,176 @@
+"""Protocol variants beyond the reference's default path: legacy majority
+election + centralised server push, the thesis verification /
+voting rules, fusion_avg with the KDE/JS similarity utilities
+(C32), and dropped-client fault injection."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from fedmse_decentralized_amd.config import ExperimentConfig
+from fedmse_decentralized_amd.federation import Federation
+from fedmse_decentralized_amd.protocol.election import elect_aggregator, elect_majority
+from fedmse_decentralized_amd.protocol.verification import ThesisVerifier, VerifierState
+from fedmse_decentralized_amd.utils import similarity as sim
+from fedmse_decentralized_amd.utils.rng_replay import HostNoise
+
+
+class NoNoise:
+    def rand(self):
+        return 0.5
+
+
+def test_majority_election_counts_votes():
+    sel = [3, 1, 4, 2]
+    scores = {3: 0.5, 1: 0.1, 4: 0.2, 2: 0.3}
+    # voters 3, 4, 2 vote for 1 (lowest); voter 1 votes for 4
+    el = elect_majority(sel, scores, [0] * 5, 3, NoNoise(), log_enabled=False)
+    assert el.aggregator == 1
+    # cap: client 1 exhausted -> 3, 2 vote 4; 4 votes 2; 1 votes 4 -> 4 wins
+    el = elect_majority(sel, scores, [0, 3, 0, 0, 0], 3, NoNoise(), log_enabled=False)
+    assert el.aggregator == 4
+
+
+def test_thesis_vote_cap_and_random_fallback():
+    sel = [0, 1, 2]
+    scores = {0: 5.0, 1: 4.0, 2: 7.0}      # every score above the cap of 3
+    el = elect_aggregator(sel, scores, [0, 0, 0], 3, NoNoise(), log_enabled=False, vote_mse_cap=3.0)
+    assert el.aggregator is None
+    el = elect_aggregator(sel, scores, [0, 3, 0], 3, NoNoise(), log_enabled=False, vote_mse_cap=3.0,
+                          fallback_rng=random.Random(0))
+    assert el.aggregator in (0, 2)
+    # below the cap the normal rule applies
+    scores = {0: 0.5, 1: 0.4, 2: 2.0}
+    el = elect_aggregator(sel, scores, [0, 0, 0], 3, NoNoise(), log_enabled=False, vote_mse_cap=3.0)
+    assert el.aggregator == 1
+
+
+def test_thesis_verifier_loss_ratio():
+    v = ThesisVerifier(ratio=0.1)
+    st = VerifierState()
+    assert v.decide_losses(0, st, 0, old_loss=1.0, new_loss=1.09, current_round=0).verified
+    assert not v.decide_losses(0, st, 1, old_loss=1.0, new_loss=1.11, current_round=1).verified
+    assert not v.decide_losses(0, st, 2, old_loss=1.0, new_loss=float("nan"), current_round=2).verified
+    assert not v.decide_losses(0, st, 3, old_loss=1.0, new_loss=float("inf"), current_round=3).verified
+
+
+def test_gaussian_divergences_closed_form():
+    rng = np.random.default_rng(0)
+    a = rng.normal(size=(3, 3))
+    cov = a @ a.T + 3 * np.eye(3)
+    mu = rng.normal(size=3)
+    assert abs(sim.kl_divergence(mu, cov, mu, cov)) < 1e-12
+    assert abs(sim.js_divergence(mu, cov, mu, cov)) < 1e-12
+    # 1-D check against the textbook formula
+    kl = sim.kl_divergence(np.array([0.0]), np.array([[1.0]]), np.array([1.0]), np.array([[2.0]]))
+    assert abs(kl - (np.log(np.sqrt(2.0)) + (1 + 1) / (2 * 2.0) - 0.5)) < 1e-12
+    assert sim.js_divergence(mu, cov, mu + 1, cov) > 0
+
+
+def test_similarity_score_and_fusion_weights():
+    rng = np.random.default_rng(1)
+    dev = rng.normal(size=(200, 4))
+    dev_kde = sim.kde_log_density(dev)
+    close = sim.similarity_score(dev_kde, dev + 0.01 * rng.normal(size=dev.shape))
+    far = sim.similarity_score(dev_kde, 5.0 * rng.normal(size=dev.shape) + 3.0)
+    assert 0 <= close < far
+    w = sim.fusion_weights([close, far])
+    assert abs(w.sum() - 1) < 1e-12 and w[0] > w[1]
+
+
+SMALL = dict(normal_rows=(90, 100), abnormal_rows=(120, 130), test_normal_rows=20)
+
+
+@pytest.fixture(autouse=True)
+def _small_synthetic(monkeypatch):
+    from fedmse_decentralized_amd.data import synthetic
+
+    orig = synthetic.SyntheticSpec.resolved
+
+    def resolved(self):
+        s = orig(self)
+        s.normal_rows, s.abnormal_rows, s.test_normal_rows = SMALL["normal_rows"], SMALL["abnormal_rows"], \
+            SMALL["test_normal_rows"]
+        return s
+    monkeypatch.setattr(synthetic.SyntheticSpec, "resolved", resolved)
+    from fedmse_decentralized_amd import federation
+    federation._PREP_CACHE.clear()
+
+
+def _cfg(tmp_path, **kw):
+    base = dict(synthetic="nbaiot", network_size=4, num_rounds=3, epoch=2, batch_size=12,
+                output_root=str(tmp_path), backend="torch", device="cpu", log_level="WARNING",
+                model_types=["hybrid"], update_types=["avg"], global_early_stop=False, save_checkpoints=False)
+    base.update(kw)
+    return ExperimentConfig(**base)
+
+
+def test_centralized_majority_mode_pushes_aggregate_to_everyone(tmp_path):
+    cfg = _cfg(tmp_path, election="majority", aggregation_mode="centralized")
+    fed = Federation(cfg, "hybrid", "avg", 0).setup()
+    r = fed.run_round()
+    assert r.aggregator is not None and r.verification == []
+    p = fed.engine.store.params
+    for c in range(1, fed.N):
+        assert torch.equal(p[c], p[0])          # every client holds the aggregate
+    assert torch.equal(fed.engine.store.anchor[0], p[0])
+
+
+def test_thesis_variant_runs(tmp_path):
+    cfg = _cfg(tmp_path, protocol_variant="thesis", num_rounds=3)
+    fed = Federation(cfg, "hybrid", "mse_avg", 0).setup()
+    for _ in range(3):
+        r = fed.run_round()
+        assert np.all(np.isfinite(r.metrics))
+        for v in r.verification:
+            assert set(v) == {"client_id", "rejected_updates", "is_verified"}
+
+
+def test_fusion_avg_runs(tmp_path):
+    cfg = _cfg(tmp_path, fusion_max_rows=128, num_rounds=2)
+    fed = Federation(cfg, "hybrid", "fusion_avg", 0).setup()
+    r = fed.run_round()
+    assert r.aggregator is not None and np.all(np.isfinite(r.metrics))
+
+
+def test_dropped_clients_no_aggregator_path(tmp_path):
+    cfg = _cfg(tmp_path, dropped_clients=[0, 1, 2, 3])
+    fed = Federation(cfg, "hybrid", "avg", 0).setup()
+    before = fed.engine.store.params.clone()
+    r = fed.run_round()
+    assert r.aggregator is None and r.selected == [] and r.verification == []
+    assert torch.equal(fed.engine.store.params, before)
+
+
+def test_peer_api_roundtrip(tmp_path):
+    """Reference ClientTrainer-style driving: run, vote, aggregate, broadcast,
+    receive, verify."""
+    cfg = _cfg(tmp_path, network_size=4)
+    fed = Federation(cfg, "hybrid", "mse_avg", 0).setup()
+    peers = fed.peers()
+    for p in peers:
+        p.connect_to_peers([q for q in peers if q is not p])
+    trk = peers[0].run()
+    assert len(trk) >= 1 and all(np.isfinite(t[0]) for t in trk)
+    s = peers[1].calculate_mse_score(fed.clients[0].valid)
+    assert s > 0
+    choice = peers[0].vote_for_aggregator(peers, fed.clients[0].valid)
+    assert choice is not None and choice is not peers[0]
+    agg = choice.aggregate_models(peers)
+    assert agg is not None and choice.aggregation_count == 1
+    assert torch.equal(choice.params(), agg)
+    choice.broadcast_model()
+    for p in peers:
+        if p is not choice:
+            assert choice.client_id in p.received_models
+            assert p.update_from_peers() is True          # first receipt is always accepted
+            assert torch.equal(p.params(), agg) and p.received_models == {}
+    # request_aggregation aggregates the inbox without loading it
+    peers[1].receive_model(peers[2], peers[2].params().clone())
+    peers[1].receive_model(peers[3], peers[3].params().clone() * 1.0)
+    before = peers[1].params().clone()
+    out = peers[1].request_aggregation()
+    assert out is not None and torch.equal(peers[1].params(), before)
+    sd = peers[1].state_dict()
+    assert list(sd)[0] == "encoder.encoder_network.0.weight"

@@ -1,0 +1,40 @@
+"""Tooling scripts on CPU: results tables from report files, rocpd profile
+summaries (on a synthetic rocpd-shaped database)."""
+import json
+import os
+import sqlite3
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+
+
+def test_results_table(tmp_path):
+    import results_table
+
+    d = tmp_path / "Run_0" / "AUC"
+    d.mkdir(parents=True)
+    with open(d / "FL-IoT_0.5_hybrid_mse_avg_results.json", "w") as f:
+        for r in range(3):
+            f.write(json.dumps({"round": r, "client_metrics": [0.9 + 0.01 * r, 0.8], "update_type": "mse_avg",
+                                "model_type": "hybrid", "global_loss": 0.8}) + "\n")
+    res = results_table.load_results(str(tmp_path))
+    t = results_table.table(res, per_round=True)
+    assert "| hybrid | mse_avg | 3 | 0.8600 | 0.8000 | 0.9200 |" in t and "99.01" in t
+
+
+def test_prof_summary_on_synthetic_db(tmp_path):
+    import prof_summary
+
+    db = tmp_path / "x.db"
+    c = sqlite3.connect(db)
+    c.execute("create table kernels (name text, start int, end int, duration int, grid_x int, grid_y int, "
+              "workgroup_x int, lds_size int, scratch_size int, vgpr_count int, accum_vgpr_count int, sgpr_count int)")
+    t = 0
+    for rnd in range(3):
+        for name, dur in (("void fedmx::train_kernel<false>(fedmx::TrainArgs)", 1000), ("fedmx::auc_kernel", 60)):
+            c.execute("insert into kernels values (?,?,?,?,?,?,?,?,?,?,?,?)",
+                      (name, t, t + dur, dur, 1280, 1, 256, 0, 0, 128, 0, 64))
+            t += dur + 10
+    c.commit()
+    s = prof_summary.summarize(str(db), "t")
+    assert "fedmx::train_kernel<false>" in s and "one round timeline" in s
