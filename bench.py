@@ -86,7 +86,7 @@ def main(argv=None):
 
     def one_round():
         if fed.round_idx and fed.round_idx % EPISODE == 0:
-            fed.agg_counts = [0] * fed.N   # new 20-round episode (fresh protocol counters)
+            fed.reset_aggregation_counts()   # new 20-round episode (fresh protocol counters)
         return fed.run_round()
 
     for _ in range(args.warmup):
@@ -104,6 +104,7 @@ def main(argv=None):
     last = None
     for _ in range(args.steps):
         last = one_round()
+    fed.finish()         # device-protocol rounds: collect results, hand reports to the writer
     fed.writer.flush()   # artefacts of the timed rounds are on disk before the clock stops
     if prof is not None:
         prof.disable()
@@ -150,6 +151,7 @@ def main(argv=None):
                 "local_epochs": args.epochs,
                 "backend": fed.engine.name,
                 "compat": args.compat,
+                "device_protocol": fed._fast is not None,
             },
             "federation_rounds_per_sec": round(fed_rps, 4),
             "detection_auc_mean": round(auc, 6),

@@ -97,6 +97,9 @@ class ExperimentConfig:
     # as a single-rank federation on that rank's GPU) instead of every
     # combination being sharded over all ranks.
     parallel_combos: bool = False
+    # fixed compat + HIP engine: run the round's protocol decisions on the
+    # device (engine/device_round.py) so rounds need no host synchronisation
+    device_protocol: bool = True
 
     # -----------------------------------------------------------------------
     @property

@@ -1,0 +1,325 @@
+"""Device-resident decentralised round (the fixed-compat fast path).
+
+The host path (``Federation.run_round``) takes the protocol decisions on the
+host and therefore synchronises with the GPU three times per round (after
+training + voting, after verification, after evaluation).  With
+``compat="fixed"`` every decision input is either on the device or drawn from
+a host RNG whose consumption does not depend on results, so the whole round
+can be *enqueued* instead:
+
+    train (fused kernel, all local selected clients)     -> best snapshot D2H (async)
+    zero report vectors; standardise vote data; forward + score_reduce -> vec[N,4]
+    [RCCL all-reduce vec]                                 (vote scores, dev MSEs)
+    elect_kernel            aggregator, cap counts, FedAvg / FedMSE weights
+    [pack + RCCL all-gather of the selected models]
+    gather_wsum_kernel      aggregate (bit-identical to the host path)
+    forward(agg, every hosted client's verification data) + score_reduce
+    param_drift(hist, agg)  per hosted client
+    decide_adopt_kernel     ModelVerifier rule + adoption + history update
+    [RCCL all-reduce rejected counts]
+    evaluation (fwd + CEN + AUC)  [RCCL all-reduce AUCs]
+    copy report vectors into a mapped per-round slot; record an event
+
+and the host moves on to the next round.  Results are *collected* later
+(at most ``max_pending`` rounds behind, or when a caller reads a round's
+fields): the mapped slots are read after the round's event, logs are
+emitted, and reports / checkpoints are handed to the background writer.
+A round therefore costs its GPU time only; the host work of round r+1
+overlaps the GPU work of round r.
+
+Decisions, aggregates and metrics are identical to the host path in fixed
+mode (tested on the GPU); the host-side RNG draws one k x (k-1) noise table
+per round in both paths.
+"""
+from __future__ import annotations
+
+import logging
+from collections import deque
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..models.layout import P_PAD
+from ..ops import _hip
+
+log = logging.getLogger("fedmx")
+
+
+def fast_path_supported(fed) -> Optional[str]:
+    """None when the device round can run this federation, else the reason it cannot."""
+    cfg = fed.cfg
+    if fed.engine.name != "hip":
+        return "engine is not the HIP engine"
+    checks = [
+        (cfg.compat == "fixed", "compat mode is not 'fixed'"),
+        (cfg.election == "first_voter", "election is not first_voter"),
+        (cfg.aggregation_mode == "decentralized", "aggregation mode is not decentralized"),
+        (cfg.protocol_variant == "code", "protocol variant is not 'code'"),
+        (fed.update_type in ("avg", "fedprox", "mse_avg"), f"update type {fed.update_type}"),
+        (cfg.metric == "AUC", "metric is not AUC"),
+        (not cfg.malicious_clients and not cfg.dropped_clients, "fault injection is enabled"),
+        (not cfg.save_latents, "latent logging is enabled"),
+        (not cfg.resume and not cfg.snapshot_every, "resume snapshots are enabled"),
+        (cfg.device_protocol, "device protocol disabled"),
+    ]
+    for ok, why in checks:
+        if not ok:
+            return why
+    return None
+
+
+class LazyRoundResult:
+    """A round whose device results are read on first access."""
+
+    def __init__(self, dr: "DeviceRound", rec: dict):
+        self._dr = dr
+        self._rec = rec
+        self.round = rec["round"]
+        self.selected = rec["selected"]
+        self.times_ms = rec.get("times_ms", {})
+
+    def _get(self, k):
+        if not self._rec["done"]:
+            self._dr.collect_until(self._rec["round"])
+        return self._rec[k]
+
+    aggregator = property(lambda self: self._get("aggregator"))
+    metrics = property(lambda self: self._get("metrics"))
+    verification = property(lambda self: self._get("verification"))
+    epochs_run = property(lambda self: self._get("epochs_run"))
+    stop = property(lambda self: self._get("stop"))
+
+
+class DeviceRound:
+    def __init__(self, fed, max_pending: int = 2):
+        self.fed = fed
+        eng = fed.engine
+        st = eng.store
+        dev = eng.device
+        self.dev = dev
+        N = fed.N
+        self.N = N
+        self.start = fed.local[0] if fed.local else 0
+        self.n_local = len(fed.local)
+        self.max_pending = max_pending
+        f64, i32, f32 = torch.float64, torch.int32, torch.float32
+        self.vec = torch.zeros(N, 4, dtype=f64, device=dev)
+        self.agg_counts = torch.zeros(N, dtype=i32, device=dev)
+        self.weights = torch.zeros(max(N, 1), dtype=f32, device=dev)
+        self.state = torch.full((4,), -1, dtype=i32, device=dev)
+        self.agg = torch.zeros(P_PAD, dtype=f32, device=dev)
+        n = max(self.n_local, 1)
+        self.hist = torch.zeros(n, P_PAD, dtype=f32, device=dev)
+        self.has_hist = torch.zeros(n, dtype=i32, device=dev)
+        self.hist_perf = torch.zeros(n, dtype=f64, device=dev)
+        self.rejected = torch.zeros(n, dtype=i32, device=dev)
+        self.mse = torch.zeros(n, 2, dtype=f64, device=dev)
+        self.drift = torch.zeros(n, dtype=f32, device=dev)
+        self.rej_vec = torch.zeros(N, dtype=f64, device=dev)
+        self.metrics = torch.zeros(N, dtype=f64, device=dev)
+        self.rt = _hip.runtime(dev)
+        cfg = fed.cfg
+        # verification: the aggregate on every hosted client's verification data (fixed mode: own V)
+        if cfg.verification_method == "dev":
+            vdata = [fed.dev_set for _ in fed.local]
+        else:
+            vdata = [fed.valid_all[c] for c in fed.local]
+        self.vplan = _hip.FwdPlan(self.agg.unsqueeze(0), [(0, d) for d in vdata], fed.dims,
+                                  want_sse=True, want_latent=False) if fed.local else None
+        if fed.local:
+            self.vseg = _hip.seg_desc_device(self.vplan.sse_views(), [0] * self.n_local,
+                                             self.mse.data_ptr() + 16 * np.arange(self.n_local), dev)
+        self.rule = 1 if fed.update_type == "mse_avg" else 0
+        self.pending: deque = deque()
+        self.all_rounds: Dict[int, dict] = {}
+        self.host_agg_counts = [0] * N
+
+    # ------------------------------------------------------------------------------
+    def reset_aggregation_counts(self):
+        self.agg_counts.zero_()
+        self.host_agg_counts = [0] * self.N
+
+    def _loc(self, c):
+        return c - self.start
+
+    def enqueue(self, selected: List[int]) -> LazyRoundResult:
+        fed = self.fed
+        cfg, eng, st, comm = fed.cfg, fed.engine, fed.engine.store, fed.comm
+        tel = fed.tel
+        N, dev = self.N, self.dev
+        rnd = fed.round_idx
+        k = len(selected)
+        local_sel = [c for c in selected if fed._mine(c)]
+        local_rows = [self._loc(c) for c in local_sel]
+        rec = dict(round=rnd, selected=list(selected), local_sel=local_sel, done=False)
+
+        with tel.phase("train"):
+            handle = eng.train_launch(local_rows, fed.hp) if local_sel else None
+            rec["handle"] = handle
+            if local_sel and cfg.save_checkpoints:
+                from ..io.async_writer import snapshot_to_host
+
+                rec["snap"] = snapshot_to_host(st.best)
+        with tel.phase("vote"):
+            self.vec.zero_()
+            self.rej_vec.zero_()
+            if local_sel:
+                vs = eng.standardized_vote_data(fed.valid_all[selected[0]])
+                need_dev = self.rule == 1
+                items = [(r, vs) for r in local_rows]
+                outs = [self.vec[c].data_ptr() for c in local_sel]
+                batch = [cfg.vote_batch_size] * len(local_rows)
+                if need_dev:
+                    items += [(r, fed.dev_set) for r in local_rows]
+                    outs += [self.vec[c].data_ptr() + 16 for c in local_sel]
+                    batch += [0] * len(local_rows)
+                sse, _ = _hip.forward_rows(st.params, items, fed.dims, True, False)
+                _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs)
+        with tel.phase("comm"):
+            comm.all_reduce_inplace(self.vec)
+        with tel.phase("vote"):
+            noise = np.array([fed.noise.rand() for _ in range(k * (k - 1))], dtype=np.float64)
+            sel_ptr, noise_ptr = self.rt.desc.put(np.asarray(selected, dtype=np.int32),
+                                                  noise if noise.size else np.zeros(1))
+            rep_ptr, rep_view = self.rt.out.take(np.int32, 2)
+            rep_view[:] = -2
+            a = _hip.ElectArgs(sel=sel_ptr, vec=self.vec.data_ptr(), noise=noise_ptr,
+                               agg_counts=self.agg_counts.data_ptr(), weights=self.weights.data_ptr(),
+                               state=self.state.data_ptr(), report=rep_ptr, k=k, cap=cfg.max_aggregation,
+                               rule=self.rule, pad=0)
+            _hip.elect(a, dev)
+            rec["report"] = rep_view
+        with tel.phase("comm"):
+            if comm.world_size == 1:
+                base = st.params
+                rows = np.asarray([self._loc(c) for c in selected], dtype=np.int64)
+            else:
+                per_rank: Dict[int, List[int]] = {}
+                for c in selected:
+                    per_rank.setdefault(fed.shard.owner(c), []).append(c)
+                slots = max(len(v) for v in per_rank.values())
+                mine = per_rank.get(comm.rank, [])
+                send = torch.zeros(slots, P_PAD, dtype=torch.float32, device=dev)
+                if mine:
+                    idx = torch.tensor([self._loc(c) for c in mine], dtype=torch.long, device=dev)
+                    send[:len(mine)] = st.params.index_select(0, idx)
+                base = comm.all_gather(send).reshape(-1, P_PAD)
+                rows = np.asarray([fed.shard.owner(c) * slots + per_rank[fed.shard.owner(c)].index(c)
+                                   for c in selected], dtype=np.int64)
+                rec["_keep"] = base
+        with tel.phase("aggregate"):
+            (rows_ptr,) = self.rt.desc.put(rows)
+            w = _hip.WsumArgs(base=base.data_ptr(), rows=rows_ptr, weights=self.weights.data_ptr(),
+                              state=self.state.data_ptr(), out=self.agg.data_ptr(), k=k, P=P_PAD)
+            _hip.gather_wsum(w, dev)
+        with tel.phase("verify"):
+            if self.n_local:
+                self.vplan.run()
+                _hip.launch_score_reduce(self.vseg, self.n_local, fed.dims.d_in, dev)
+                _hip._check(_hip.lib().fedmx_param_drift(self.hist.data_ptr(), self.n_local, self.agg.data_ptr(),
+                                                         eng._seg.data_ptr(), self.drift.data_ptr(), self.rt.stream),
+                            "fedmx_param_drift")
+                d = _hip.DecideArgs(params=st.params.data_ptr(), anchor=st.anchor.data_ptr(),
+                                    hist=self.hist.data_ptr(), agg=self.agg.data_ptr(), state=self.state.data_ptr(),
+                                    mse=self.mse.data_ptr(), drift=self.drift.data_ptr(),
+                                    has_hist=self.has_hist.data_ptr(), hist_perf=self.hist_perf.data_ptr(),
+                                    rejected=self.rejected.data_ptr(), rej_vec=self.rej_vec.data_ptr(),
+                                    thr=float(cfg.verification_threshold), pthr=float(cfg.performance_threshold),
+                                    start=self.start, n_local=self.n_local, P=P_PAD, pad=0)
+                _hip.decide_adopt(d, dev)
+        with tel.phase("comm"):
+            comm.all_reduce_inplace(self.rej_vec)
+        with tel.phase("eval"):
+            self.metrics.zero_()
+            aucs = eng.evaluate_launch(fed.model_type)
+            plan = eng._eval_plans[fed.model_type]
+            if self.n_local:
+                _hip.copy_f64(self.metrics.data_ptr() + 8 * self.start, plan["aucs_buf"].dev_ptr, self.n_local, dev)
+        with tel.phase("comm"):
+            comm.all_reduce_inplace(self.metrics)
+        slot_ptr, slot = self.rt.out.take(np.float64, 2 * N)
+        _hip.copy_f64(slot_ptr, self.metrics.data_ptr(), N, dev)
+        _hip.copy_f64(slot_ptr + 8 * N, self.rej_vec.data_ptr(), N, dev)
+        rec["slot"] = slot
+        ev = torch.cuda.Event()
+        ev.record()
+        rec["event"] = ev
+        fed.round_idx += 1
+        rec["times_ms"] = tel.end_round(round=rnd + 1, selected=k, aggregator=None)
+        self.pending.append(rec)
+        self.all_rounds[rnd] = rec
+        res = LazyRoundResult(self, rec)
+        # bounded run-ahead: collect rounds that are max_pending behind (normally already finished)
+        while len(self.pending) > self.max_pending:
+            self._collect(self.pending.popleft())
+        if cfg.global_early_stop:
+            self.collect_until(rnd)
+        return res
+
+    # ------------------------------------------------------------------------------
+    def collect_until(self, rnd: int):
+        while self.pending and self.pending[0]["round"] <= rnd:
+            self._collect(self.pending.popleft())
+
+    def collect_all(self):
+        while self.pending:
+            self._collect(self.pending.popleft())
+
+    def _collect(self, rec: dict):
+        fed = self.fed
+        cfg, eng = fed.cfg, fed.engine
+        rec["event"].synchronize()
+        N = self.N
+        rnd = rec["round"]
+        info = log.isEnabledFor(logging.INFO)
+        agg = int(rec["report"][0])
+        aggregator = agg if agg >= 0 else None
+        slot = rec["slot"]
+        metrics = np.array(slot[:N], dtype=np.float64)
+        rej = np.array(slot[N:2 * N], dtype=np.float64)
+        if bool(np.any(metrics == -1.0)):
+            raise RuntimeError("device AUC reported a class too large for the LDS sort; disable the device "
+                               "protocol (--device-protocol false) for this dataset")
+        handle = rec.get("handle")
+        epochs_local: Dict[int, int] = {}
+        if handle is not None:
+            res = eng.train_collect(handle, [np.array(t) for t in handle.tensors])
+            for i, c in enumerate(rec["local_sel"]):
+                epochs_local[c] = int(res.epochs_run[i])
+                if info:
+                    for e, (tl, vl) in enumerate(res.tracking[i]):
+                        log.info(f"[Client {c}] Epoch {e + 1} - Training loss: {tl} - Validating loss: {vl}")
+            if cfg.save_checkpoints:
+                snap, ev = rec["snap"]
+                fed._submit_checkpoints(res, rec["local_sel"], snap, ev)
+        verification = []
+        if aggregator is not None:
+            self.host_agg_counts[aggregator] += 1
+            fed.agg_counts[aggregator] += 1
+            if info:
+                log.info(f"Client {aggregator + 1} selected as aggregator")
+            for c in range(N):
+                if c != aggregator:
+                    r = int(rej[c])
+                    verification.append({"client_id": c, "rejected_updates": r, "is_verified": r == 0})
+            if fed.write_reports:
+                vr = verification
+                fed.writer.submit(lambda vr=vr, rnd=rnd: fed._report_verification(rnd, vr))
+        else:
+            log.warning("No aggregator selected for this round")
+        if info:
+            for i in range(N):
+                log.info(f"Client {i + 1} {cfg.metric} score: {metrics[i]}")
+        if fed.write_reports:
+            m_ = metrics.copy()
+            fed.writer.submit(lambda m_=m_, rnd=rnd: fed._report_round(rnd, m_))
+        fed.last_metrics = metrics
+        stop = False
+        if cfg.global_early_stop:
+            stop = fed.early.update(float(np.min(metrics)))
+        rec.update(aggregator=aggregator, metrics=metrics, verification=verification, epochs_run=epochs_local,
+                   stop=stop, done=True)
+        for key in ("handle", "snap", "slot", "report", "_keep", "event"):
+            rec.pop(key, None)
+        self.all_rounds.pop(rnd, None)

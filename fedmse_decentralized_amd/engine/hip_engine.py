@@ -107,15 +107,20 @@ class HipEngine(Engine):
         return _hip.standardize_ddof1(x.contiguous(), self.dims.d_in)
 
     # -- round operations ------------------------------------------------------------
+    def standardized_vote_data(self, vote_data):
+        """Vote data standardised (ddof 1) into a persistent device buffer (stream-ordered reuse)."""
+        if self._vs is None or self._vs.shape[0] < vote_data.shape[0]:
+            self._vs = torch.empty(max(vote_data.shape[0], 256), 128, dtype=torch.float32, device=self.device)
+        vs = self._vs[:vote_data.shape[0]]
+        _hip.standardize_ddof1(vote_data.contiguous(), self.dims.d_in, out=vs)
+        return vs
+
     def vote_scores(self, local_rows, vote_data, dev_set, vote_bs):
         """Host view [k, 2] (vote score, dev MSE) written by the kernels."""
         k = len(local_rows)
         if k == 0:
             return np.zeros((0, 2), dtype=np.float64)
-        if self._vs is None or self._vs.shape[0] < vote_data.shape[0]:
-            self._vs = torch.empty(max(vote_data.shape[0], 256), 128, dtype=torch.float32, device=self.device)
-        vs = self._vs[:vote_data.shape[0]]
-        _hip.standardize_ddof1(vote_data.contiguous(), self.dims.d_in, out=vs)
+        vs = self.standardized_vote_data(vote_data)
         items = [(c, vs) for c in local_rows]
         if dev_set is not None:
             items += [(c, dev_set) for c in local_rows]

@@ -115,6 +115,19 @@ class RoundResult:
     times_ms: Dict[str, float] = field(default_factory=dict)
 
 
+class _TableNoise:
+    """Noise source replaying a pre-drawn table (fixed-compat election)."""
+
+    def __init__(self, table):
+        self.table = table
+        self.i = 0
+
+    def rand(self) -> float:
+        v = self.table[self.i]
+        self.i += 1
+        return v
+
+
 class Federation:
     def __init__(self, cfg: ExperimentConfig, model_type: str, update_type: str, run: int,
                  comm: Optional[Comm] = None, device: Optional[torch.device] = None,
@@ -185,7 +198,48 @@ class Federation:
                 os.makedirs(d, exist_ok=True)
         if cfg.resume:
             self.restore(ckpt.load_resume(self._resume_path(cfg.resume)))
+        self._fast = None
+        from .engine.device_round import DeviceRound, fast_path_supported
+
+        why = fast_path_supported(self)
+        if why is None:
+            self._fast = DeviceRound(self)
+        else:
+            log.debug(f"device protocol off: {why}")
         return self
+
+    def reset_aggregation_counts(self) -> None:
+        """New protocol episode: every client may aggregate max_aggregation times again."""
+        self.agg_counts = [0] * self.N
+        if self._fast is not None:
+            self._fast.reset_aggregation_counts()
+
+    def finish(self) -> None:
+        """Collect every enqueued device round (reports handed to the writer)."""
+        if getattr(self, "_fast", None) is not None:
+            self._fast.collect_all()
+
+    # -- report / artefact submission (background writer) ---------------------------
+    def _report_round(self, rnd: int, metrics: np.ndarray) -> None:
+        reports.append_round_result(self.cfg, self.run, rnd, metrics, self.model_type, self.update_type)
+
+    def _report_verification(self, rnd: int, vr: List[Dict]) -> None:
+        reports.append_verification(self.cfg, self.run, rnd, vr)
+
+    def _submit_checkpoints(self, res, local_sel: Sequence[int], snap, ev) -> None:
+        dims = self.dims
+        cidx = self._canon_idx
+        for i, c in enumerate(local_sel):
+            d = self.save_dirs[c]
+            row = self._loc(c)
+            improved = res.best_epoch[i] >= 0
+            trk = list(res.tracking[i])
+
+            def job(d=d, row=row, improved=improved, trk=trk):
+                if improved:
+                    ckpt.save_model_cpt_fast(d, snap[row].numpy()[cidx], dims)
+                ckpt.save_tracking(d, trk)
+            self.writer.submit(job, ev)
 
     def _resume_path(self, base: str) -> str:
         return base if self.comm.world_size == 1 else f"{base}.rank{self.comm.rank}"
@@ -229,21 +283,8 @@ class Federation:
         """model.cpt (best-validation snapshot of this round's training) and
         training_tracking.pkl per trained client, written by the background
         writer from an asynchronous device->pinned copy."""
-        st = self.engine.store
-        snap, ev = snapshot_to_host(st.best)
-        dims = self.dims
-        cidx = self._canon_idx
-        for i, c in enumerate(local_sel):
-            d = self.save_dirs[c]
-            row = self._loc(c)
-            improved = res.best_epoch[i] >= 0
-            trk = list(res.tracking[i])
-
-            def job(d=d, row=row, improved=improved, trk=trk):
-                if improved:
-                    ckpt.save_model_cpt_fast(d, snap[row].numpy()[cidx], dims)
-                ckpt.save_tracking(d, trk)
-            self.writer.submit(job, ev)
+        snap, ev = snapshot_to_host(self.engine.store.best)
+        self._submit_checkpoints(res, local_sel, snap, ev)
 
     # -- one round ---------------------------------------------------------------
     def run_round(self) -> RoundResult:
@@ -256,6 +297,8 @@ class Federation:
 
         with self.tel.phase("select"):
             selected = select_clients(self.py_rng, N, cfg.num_participants)
+            if self._fast is not None:
+                return self._fast.enqueue(selected)
             if cfg.dropped_clients:   # fault injection: offline clients neither train, vote nor aggregate
                 selected = [c for c in selected if c not in cfg.dropped_clients]
             local_sel = [c for c in selected if self._mine(c)]
@@ -310,7 +353,13 @@ class Federation:
             self.noise.iterators(2 * sum(epochs_all.values()))
             elect = elect_majority if cfg.election == "majority" else elect_aggregator
             cap = cfg.thesis_vote_mse_cap if cfg.protocol_variant == "thesis" else None
-            el = elect(selected, base_scores, self.agg_counts, cfg.max_aggregation, self.noise,
+            noise = self.noise
+            if cfg.compat == "fixed":
+                # one k x (k-1) table per round, drawn whatever the outcome (the
+                # device protocol draws the same table)
+                k = len(selected)
+                noise = _TableNoise([self.noise.rand() for _ in range(k * (k - 1))])
+            el = elect(selected, base_scores, self.agg_counts, cfg.max_aggregation, noise,
                        log_enabled=info, vote_mse_cap=cap, fallback_rng=self.fallback_rng)
             aggregator = el.aggregator
 
@@ -319,7 +368,7 @@ class Federation:
             if info:
                 log.info(f"Client {aggregator + 1} selected as aggregator")
             with self.tel.phase("aggregate"):
-                if self.update_type == "mse_avg":
+                if self.update_type == "mse_avg" and cfg.compat == "reference":
                     for _ in selected:          # calculate_mse_score per client (weights unused, Q3)
                         self.noise.rand()
                 sim = None
@@ -354,7 +403,7 @@ class Federation:
                         log.info(f"Client {r_['client_id']}: {'Verified' if r_['is_verified'] else 'Rejected'} "
                                  f"(Rejected updates: {r_['rejected_updates']})")
                 vr = verification_results
-                self.writer.submit(lambda vr=vr, rnd=rnd: reports.append_verification(cfg, self.run, rnd, vr))
+                self.writer.submit(lambda vr=vr, rnd=rnd: self._report_verification(rnd, vr))
         else:
             log.warning("No aggregator selected for this round")
 
@@ -376,8 +425,7 @@ class Federation:
             self.latent_log[rnd] = {n: l for n, l in zip(names, er.latents)}
         if self.write_reports:
             m_ = metrics.copy()
-            self.writer.submit(lambda m_=m_, rnd=rnd: reports.append_round_result(
-                cfg, self.run, rnd, m_, self.model_type, self.update_type))
+            self.writer.submit(lambda m_=m_, rnd=rnd: self._report_round(rnd, m_))
         self.last_metrics = metrics
         stop = False
         if cfg.global_early_stop:
@@ -497,8 +545,9 @@ class Federation:
             r = self.run_round()
             if cfg.snapshot_every and self.round_idx % cfg.snapshot_every == 0:
                 self.save_snapshot()
-            if r.stop:
+            if cfg.global_early_stop and r.stop:
                 break
+        self.finish()
         if self.last_metrics is None:
             er = self.engine.evaluate(self.model_type, cfg.metric)
             vec = torch.zeros(self.N, dtype=torch.float64)

@@ -64,6 +64,25 @@ class TrainArgs(ctypes.Structure):
     ]
 
 
+_vp, _i32 = ctypes.c_void_p, ctypes.c_int32
+
+
+class ElectArgs(ctypes.Structure):
+    _fields_ = [("sel", _vp), ("vec", _vp), ("noise", _vp), ("agg_counts", _vp), ("weights", _vp), ("state", _vp),
+                ("report", _vp), ("k", _i32), ("cap", _i32), ("rule", _i32), ("pad", _i32)]
+
+
+class WsumArgs(ctypes.Structure):
+    _fields_ = [("base", _vp), ("rows", _vp), ("weights", _vp), ("state", _vp), ("out", _vp), ("k", _i32), ("P", _i32)]
+
+
+class DecideArgs(ctypes.Structure):
+    _fields_ = [("params", _vp), ("anchor", _vp), ("hist", _vp), ("agg", _vp), ("state", _vp), ("mse", _vp),
+                ("drift", _vp), ("has_hist", _vp), ("hist_perf", _vp), ("rejected", _vp), ("rej_vec", _vp),
+                ("thr", ctypes.c_double), ("pthr", ctypes.c_double), ("start", _i32), ("n_local", _i32),
+                ("P", _i32), ("pad", _i32)]
+
+
 def lib():
     global _lib
     if _lib is not None:
@@ -88,6 +107,11 @@ def lib():
                 "fedmx_broadcast_rows": [vp, vp, vp, i32, vp, i32, vp],
                 "fedmx_train": [ctypes.POINTER(TrainArgs), i32, vp],
                 "fedmx_probe_mfma": [vp, vp],
+                "fedmx_elect": [ctypes.POINTER(ElectArgs), vp],
+                "fedmx_gather_wsum": [ctypes.POINTER(WsumArgs), vp],
+                "fedmx_decide_adopt": [ctypes.POINTER(DecideArgs), vp],
+                "fedmx_copy_f64": [vp, vp, i32, vp],
+                "fedmx_protocol_sizes": [vp],
             }
             for name, args in sig.items():
                 f = getattr(L, name)
@@ -98,6 +122,9 @@ def lib():
             assert L.fedmx_auc_desc_size() == AUC_DTYPE.itemsize
             assert L.fedmx_seg_desc_size() == SEG_DTYPE.itemsize
             assert L.fedmx_train_args_size() == ctypes.sizeof(TrainArgs)
+            sz = (ctypes.c_int * 3)()
+            L.fedmx_protocol_sizes(ctypes.cast(sz, ctypes.c_void_p))
+            assert tuple(sz) == (ctypes.sizeof(ElectArgs), ctypes.sizeof(WsumArgs), ctypes.sizeof(DecideArgs)), tuple(sz)
             _lib = L
     return _lib
 
@@ -299,6 +326,50 @@ def score_reduce(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in: i
     (dptr,) = rt.desc.put(desc)
     _check(lib().fedmx_score_reduce(dptr, len(desc), d_in, rt.stream), "fedmx_score_reduce")
     return view.reshape(len(sse_list), 2)
+
+
+def score_reduce_to(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in: int, out_ptrs: Sequence[int]):
+    """score_reduce writing each segment's (vote score, MSE) pair to the given
+    device addresses (16 bytes each) instead of the result ring."""
+    dev = sse_list[0].device
+    rt = runtime(dev)
+    desc = np.zeros(len(sse_list), dtype=SEG_DTYPE)
+    desc["sse"] = [s.data_ptr() for s in sse_list]
+    desc["n"] = [int(s.shape[0]) for s in sse_list]
+    desc["batch"] = list(batch)
+    desc["out"] = np.asarray(out_ptrs, dtype=np.int64)
+    (dptr,) = rt.desc.put(desc)
+    _check(lib().fedmx_score_reduce(dptr, len(desc), d_in, rt.stream), "fedmx_score_reduce")
+
+
+def seg_desc_device(sse_list: Sequence[torch.Tensor], batch: Sequence[int], out_ptrs: Sequence[int], dev) -> torch.Tensor:
+    """A persistent score_reduce descriptor array in device memory (cached launch plans)."""
+    desc = np.zeros(len(sse_list), dtype=SEG_DTYPE)
+    desc["sse"] = [s.data_ptr() for s in sse_list]
+    desc["n"] = [int(s.shape[0]) for s in sse_list]
+    desc["batch"] = list(batch)
+    desc["out"] = np.asarray(out_ptrs, dtype=np.int64)
+    return torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+
+
+def launch_score_reduce(desc_dev: torch.Tensor, n: int, d_in: int, device):
+    _check(lib().fedmx_score_reduce(desc_dev.data_ptr(), n, d_in, _stream(device)), "fedmx_score_reduce")
+
+
+def elect(args: ElectArgs, device):
+    _check(lib().fedmx_elect(ctypes.byref(args), _stream(device)), "fedmx_elect")
+
+
+def gather_wsum(args: WsumArgs, device):
+    _check(lib().fedmx_gather_wsum(ctypes.byref(args), _stream(device)), "fedmx_gather_wsum")
+
+
+def decide_adopt(args: DecideArgs, device):
+    _check(lib().fedmx_decide_adopt(ctypes.byref(args), _stream(device)), "fedmx_decide_adopt")
+
+
+def copy_f64(dst_ptr: int, src_ptr: int, n: int, device):
+    _check(lib().fedmx_copy_f64(dst_ptr, src_ptr, n, _stream(device)), "fedmx_copy_f64")
 
 
 def broadcast_rows(dst0: torch.Tensor, dst1: Optional[torch.Tensor], rows: Sequence[int], src: torch.Tensor):

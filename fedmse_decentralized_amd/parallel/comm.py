@@ -55,6 +55,11 @@ class Comm:
     def all_gather_object(self, obj: Any) -> List[Any]:
         raise NotImplementedError
 
+    def all_reduce_inplace(self, t: torch.Tensor) -> None:
+        """In-place sum over ranks, stream-ordered on the tensor's device (no
+        host synchronisation with RCCL)."""
+        t.copy_(self.all_reduce_sum(t))
+
 
 def _np_wrap(fn):
     """Let a tensor collective also take / return numpy arrays (host protocol vectors)."""
@@ -87,6 +92,9 @@ class LoopbackComm(Comm):
 
     def all_gather_object(self, obj):
         return [obj]
+
+    def all_reduce_inplace(self, t):
+        pass
 
 
 class _ThreadGroup:
@@ -178,6 +186,12 @@ class TorchDistComm(Comm):
         x = self._to(t).clone()
         self.dist.broadcast(x, src)
         return x.to(t.device)
+
+    def all_reduce_inplace(self, t):
+        if t.device == self.device:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        else:
+            t.copy_(self.all_reduce_sum(t))
 
     def barrier(self):
         if self.backend == "nccl":

@@ -38,8 +38,11 @@ def init_comm(backend: Optional[str] = None, device: Optional[str] = None, timeo
     if backend is None:
         backend = "nccl" if device == "cuda" else "gloo"
     if device == "cuda":
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        # FEDMX_DEVICE_INDEX pins every rank to one GPU (multi-rank tests on a
+        # one-GPU box, with the gloo backend; RCCL needs distinct GPUs)
+        idx = int(os.environ.get("FEDMX_DEVICE_INDEX", local_rank))
+        torch.cuda.set_device(idx)
+        dev = torch.device("cuda", idx)
     else:
         dev = torch.device("cpu")
     if not dist.is_initialized():

@@ -1,0 +1,136 @@
+"""The device-resident round (engine/device_round.py) against the host-decision
+path on the same GPU: identical aggregators, verification results, metrics,
+parameters and report files (fixed compat), single rank and two gloo ranks
+sharing one GPU."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+from fedmse_decentralized_amd.config import ExperimentConfig
+
+SHRINK = dict(normal_rows=(150, 170), abnormal_rows=(200, 220), test_normal_rows=30)
+
+
+def _shrink():
+    from fedmse_decentralized_amd.data import synthetic
+
+    if getattr(synthetic.SyntheticSpec, "_fedmx_shrunk", False):
+        return
+    orig = synthetic.SyntheticSpec.resolved
+
+    def resolved(self):
+        s = orig(self)
+        s.normal_rows, s.abnormal_rows, s.test_normal_rows = SHRINK["normal_rows"], SHRINK["abnormal_rows"], \
+            SHRINK["test_normal_rows"]
+        return s
+    synthetic.SyntheticSpec.resolved = resolved
+    synthetic.SyntheticSpec._fedmx_shrunk = True
+
+
+def _cfg(out, **kw):
+    base = dict(synthetic="nbaiot", network_size=6, num_rounds=6, epoch=2, batch_size=12, output_root=out,
+                backend="hip", device="cuda", log_level="WARNING", compat="fixed", global_early_stop=False,
+                save_checkpoints=True, model_types=["hybrid"], update_types=["mse_avg"])
+    base.update(kw)
+    return ExperimentConfig(**base)
+
+
+def _run(cfg, update_type, rounds, comm=None):
+    from fedmse_decentralized_amd import federation
+    from fedmse_decentralized_amd.federation import Federation
+
+    federation._PREP_CACHE.clear()
+    fed = Federation(cfg, "hybrid", update_type, 0, comm=comm).setup()
+    rs = [fed.run_round() for _ in range(rounds)]
+    fed.finish()
+    fed.writer.flush()
+    out = dict(agg=[r.aggregator for r in rs], metrics=[r.metrics.tolist() for r in rs],
+               ver=[r.verification for r in rs], sel=[r.selected for r in rs])
+    torch.cuda.synchronize()
+    return fed, out
+
+
+@pytest.mark.parametrize("update_type", ["mse_avg", "avg"])
+def test_device_round_matches_host_path(tmp_path, update_type):
+    _shrink()
+    fa, a = _run(_cfg(str(tmp_path / "dev"), device_protocol=True), update_type, 6)
+    fb, b = _run(_cfg(str(tmp_path / "host"), device_protocol=False), update_type, 6)
+    assert fa._fast is not None and fb._fast is None
+    assert a["sel"] == b["sel"]
+    assert a["agg"] == b["agg"]
+    assert a["ver"] == b["ver"]
+    for x, y in zip(a["metrics"], b["metrics"]):
+        np.testing.assert_array_equal(np.array(x), np.array(y))
+    assert torch.equal(fa.engine.store.params, fb.engine.store.params)
+    assert torch.equal(fa.engine.store.anchor, fb.engine.store.anchor)
+    assert fa.agg_counts == fb.agg_counts
+    # identical report files
+    for root_a, _, files in os.walk(str(tmp_path / "dev")):
+        for fn in files:
+            if fn.endswith(".json"):
+                pa = os.path.join(root_a, fn)
+                pb = pa.replace(str(tmp_path / "dev"), str(tmp_path / "host"))
+                assert open(pa).read() == open(pb).read(), fn
+
+
+def test_device_round_early_stop_and_episode_reset(tmp_path):
+    _shrink()
+    cfg = _cfg(str(tmp_path), global_early_stop=True, num_rounds=8)
+    from fedmse_decentralized_amd import federation
+    from fedmse_decentralized_amd.federation import Federation
+
+    federation._PREP_CACHE.clear()
+    fed = Federation(cfg, "hybrid", "avg", 0).setup()
+    assert fed._fast is not None
+    fed.run_all()
+    assert 1 <= fed.round_idx <= 8
+    fed.reset_aggregation_counts()
+    assert int(fed._fast.agg_counts.sum()) == 0
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), FEDMX_DEVICE_INDEX="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    _shrink()
+    from fedmse_decentralized_amd.parallel.launch import init_comm, shutdown
+
+    comm = init_comm(backend="gloo", device="cuda")
+    fed, res = _run(_cfg(os.path.join(out, f"r{rank}"), save_checkpoints=False), "mse_avg", 4, comm=comm)
+    res["fast"] = fed._fast is not None
+    res["params"] = fed.engine.store.params.double().sum(1).tolist()
+    res["local"] = fed.local
+    with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
+        json.dump(res, f)
+    shutdown(comm)
+
+
+@pytest.mark.timeout(600)
+def test_device_round_two_ranks_one_gpu(tmp_path):
+    out = str(tmp_path)
+    mp.start_processes(_worker, args=(2, _port(), out), nprocs=2, join=True, start_method="spawn")
+    _shrink()
+    fed, ref = _run(_cfg(os.path.join(out, "single"), save_checkpoints=False), "mse_avg", 4)
+    ref_params = fed.engine.store.params.double().sum(1).tolist()
+    for r in range(2):
+        d = json.load(open(os.path.join(out, f"rank{r}.json")))
+        assert d["fast"]
+        assert d["agg"] == ref["agg"] and d["sel"] == ref["sel"] and d["ver"] == ref["ver"]
+        for x, y in zip(d["metrics"], ref["metrics"]):
+            np.testing.assert_array_equal(np.array(x), np.array(y))
+        loc = d["local"]
+        assert d["params"] == ref_params[loc[0]:loc[-1] + 1]
