@@ -119,6 +119,13 @@ class ExperimentConfig:
         return os.path.join(self.output_root, f"Checkpoint/{self.network_size}/{self.experiment_name}/{run}/ClientModel",
                             self.scen_name, model_type, update_type, device_name)
 
+    def resolved_device(self) -> str:
+        if self.device == "auto":
+            import torch
+
+            return "cuda" if torch.cuda.is_available() else "cpu"
+        return self.device
+
     def to_json(self) -> str:
         return json.dumps(dataclasses.asdict(self), indent=2, sort_keys=True)
 

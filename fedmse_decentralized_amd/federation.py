@@ -138,6 +138,8 @@ class Federation:
         self.model_type = model_type
         self.update_type = update_type
         self.run = run
+        if comm is None and device is None:
+            device = cfg.resolved_device()
         self.comm = comm or LoopbackComm(device)
         self.device = torch.device(device) if device is not None else self.comm.device
         self.dims = ModelDims(cfg.dim_features, cfg.hidden_neus, cfg.latent_dim)
