@@ -104,7 +104,12 @@ class DeviceRound:
         self.n_local = len(fed.local)
         self.max_pending = max_pending
         f64, i32, f32 = torch.float64, torch.int32, torch.float32
-        self.vec = torch.zeros(N, 4, dtype=f64, device=dev)
+        # one buffer for the per-round report vectors: a single fill per round
+        # when ranks sum them (single rank: every entry read is rewritten each round)
+        self.red = torch.zeros(6 * N, dtype=f64, device=dev)
+        self.vec = self.red[:4 * N].view(N, 4)
+        self.rej_vec = self.red[4 * N:5 * N]
+        self.metrics = self.red[5 * N:]
         self.agg_counts = torch.zeros(N, dtype=i32, device=dev)
         self.weights = torch.zeros(max(N, 1), dtype=f32, device=dev)
         self.state = torch.full((4,), -1, dtype=i32, device=dev)
@@ -116,8 +121,6 @@ class DeviceRound:
         self.rejected = torch.zeros(n, dtype=i32, device=dev)
         self.mse = torch.zeros(n, 2, dtype=f64, device=dev)
         self.drift = torch.zeros(n, dtype=f32, device=dev)
-        self.rej_vec = torch.zeros(N, dtype=f64, device=dev)
-        self.metrics = torch.zeros(N, dtype=f64, device=dev)
         self.rt = _hip.runtime(dev)
         cfg = fed.cfg
         # verification: the aggregate on every hosted client's verification data (fixed mode: own V)
@@ -162,8 +165,8 @@ class DeviceRound:
 
                 rec["snap"] = snapshot_to_host(st.best)
         with tel.phase("vote"):
-            self.vec.zero_()
-            self.rej_vec.zero_()
+            if comm.world_size > 1:
+                self.red.zero_()
             if local_sel:
                 vs = eng.standardized_vote_data(fed.valid_all[selected[0]])
                 need_dev = self.rule == 1
@@ -231,16 +234,17 @@ class DeviceRound:
         with tel.phase("comm"):
             comm.all_reduce_inplace(self.rej_vec)
         with tel.phase("eval"):
-            self.metrics.zero_()
-            aucs = eng.evaluate_launch(fed.model_type)
-            plan = eng._eval_plans[fed.model_type]
-            if self.n_local:
-                _hip.copy_f64(self.metrics.data_ptr() + 8 * self.start, plan["aucs_buf"].dev_ptr, self.n_local, dev)
-        with tel.phase("comm"):
-            comm.all_reduce_inplace(self.metrics)
+            eng.evaluate_launch(fed.model_type)
+            aucs_ptr = eng._eval_plans[fed.model_type]["aucs_buf"].dev_ptr
         slot_ptr, slot = self.rt.out.take(np.float64, 2 * N)
-        _hip.copy_f64(slot_ptr, self.metrics.data_ptr(), N, dev)
-        _hip.copy_f64(slot_ptr + 8 * N, self.rej_vec.data_ptr(), N, dev)
+        if comm.world_size == 1:
+            _hip.copy2_f64(slot_ptr, aucs_ptr, N, slot_ptr + 8 * N, self.rej_vec.data_ptr(), N, dev)
+        else:
+            if self.n_local:
+                _hip.copy_f64(self.metrics.data_ptr() + 8 * self.start, aucs_ptr, self.n_local, dev)
+            with tel.phase("comm"):
+                comm.all_reduce_inplace(self.metrics)
+            _hip.copy2_f64(slot_ptr, self.metrics.data_ptr(), N, slot_ptr + 8 * N, self.rej_vec.data_ptr(), N, dev)
         rec["slot"] = slot
         ev = torch.cuda.Event()
         ev.record()

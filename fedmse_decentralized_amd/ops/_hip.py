@@ -111,6 +111,7 @@ def lib():
                 "fedmx_gather_wsum": [ctypes.POINTER(WsumArgs), vp],
                 "fedmx_decide_adopt": [ctypes.POINTER(DecideArgs), vp],
                 "fedmx_copy_f64": [vp, vp, i32, vp],
+                "fedmx_copy2_f64": [vp, vp, i32, vp, vp, i32, vp],
                 "fedmx_protocol_sizes": [vp],
             }
             for name, args in sig.items():
@@ -370,6 +371,10 @@ def decide_adopt(args: DecideArgs, device):
 
 def copy_f64(dst_ptr: int, src_ptr: int, n: int, device):
     _check(lib().fedmx_copy_f64(dst_ptr, src_ptr, n, _stream(device)), "fedmx_copy_f64")
+
+
+def copy2_f64(d0: int, s0: int, n0: int, d1: int, s1: int, n1: int, device):
+    _check(lib().fedmx_copy2_f64(d0, s0, n0, d1, s1, n1, _stream(device)), "fedmx_copy2_f64")
 
 
 def broadcast_rows(dst0: torch.Tensor, dst1: Optional[torch.Tensor], rows: Sequence[int], src: torch.Tensor):

@@ -8,7 +8,7 @@
 //            in float64; reproduced operation by operation.
 // auc: sklearn roc_curve + auc (src/Evaluator/evaluator.py:21-28) — the area
 //   under the tie-aware ROC equals the Mann-Whitney statistic with ties
-//   counted 1/2.  One workgroup per client: the smaller class is bitonic-sorted
+//   counted 1/2.  One 1024-thread workgroup per client: the smaller class is bitonic-sorted
 //   in LDS (<= 8192 keys), every element of the other class binary-searches
 //   it, integer counts are reduced exactly.
 #include "fedmx_common.h"
@@ -98,7 +98,9 @@ __global__ __launch_bounds__(256) void cen_score_kernel(const CenDesc* __restric
     }
   }
   __syncthreads();
-  for (int r = tid; r < d.n_test; r += blockDim.x) {
+  // test rows are split over gridDim.y workgroups per client (each refits the
+  // tiny train statistics above)
+  for (int r = blockIdx.y * blockDim.x + tid; r < d.n_test; r += blockDim.x * gridDim.y) {
     double acc = 0.0;
     for (int j = 0; j < d.latent; ++j) {
       const float t0 = (float)((double)d.test_lat[(size_t)r * d.stride + j] - s_mean[j]);
@@ -138,7 +140,7 @@ __device__ __forceinline__ double load_score(const AucDesc& d, int i) {
   return clean((double)f);
 }
 
-__global__ __launch_bounds__(256) void auc_kernel(const AucDesc* __restrict__ descs) {
+__global__ __launch_bounds__(1024) void auc_kernel(const AucDesc* __restrict__ descs) {
   const AucDesc d = descs[blockIdx.x];
   extern __shared__ double keys[];  // [AUC_MAX_SORT]
   __shared__ int s_cnt[2];
@@ -237,7 +239,7 @@ extern "C" {
 
 int fedmx_cen_score(const void* descs, int n, hipStream_t stream) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(fedmx::cen_score_kernel, dim3(n), dim3(256), 0, stream,
+  hipLaunchKernelGGL(fedmx::cen_score_kernel, dim3(n, 8), dim3(256), 0, stream,
                      reinterpret_cast<const fedmx::CenDesc*>(descs));
   return (int)hipGetLastError();
 }
@@ -252,7 +254,7 @@ int fedmx_auc(const void* descs, int n, hipStream_t stream) {
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(fedmx::auc_kernel, dim3(n), dim3(256), fedmx::AUC_MAX_SORT * sizeof(double), stream,
+  hipLaunchKernelGGL(fedmx::auc_kernel, dim3(n), dim3(1024), fedmx::AUC_MAX_SORT * sizeof(double), stream,
                      reinterpret_cast<const fedmx::AucDesc*>(descs));
   return (int)hipGetLastError();
 }

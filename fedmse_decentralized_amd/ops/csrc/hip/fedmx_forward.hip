@@ -183,10 +183,10 @@ __global__ __launch_bounds__(256) void weighted_sum_kernel(const float* __restri
 // param_drift: out[m] = sum_t || hist[m] - new ||_2 over the 8 state-dict
 // tensors t (src/Trainer/model_verifier.py:79-84).  seg[p] = tensor id of
 // padded slot p (-1 = padding).  One workgroup per history vector.
-__global__ __launch_bounds__(256) void param_drift_kernel(const float* __restrict__ hist,
-                                                          const float* __restrict__ newp,
-                                                          const int* __restrict__ seg, float* __restrict__ out) {
-  __shared__ float part[8][4];
+__global__ __launch_bounds__(1024) void param_drift_kernel(const float* __restrict__ hist,
+                                                           const float* __restrict__ newp,
+                                                           const int* __restrict__ seg, float* __restrict__ out) {
+  __shared__ float part[8][16];
   const float* h = hist + (size_t)blockIdx.x * P_PAD;
   float acc[8];
 #pragma unroll
@@ -205,8 +205,13 @@ __global__ __launch_bounds__(256) void param_drift_kernel(const float* __restric
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    const int nw = blockDim.x >> 6;
     float tot = 0.f;
-    for (int t = 0; t < 8; ++t) tot += sqrtf(part[t][0] + part[t][1] + part[t][2] + part[t][3]);
+    for (int t = 0; t < 8; ++t) {
+      float s2 = 0.f;
+      for (int w = 0; w < nw; ++w) s2 += part[t][w];
+      tot += sqrtf(s2);
+    }
     out[blockIdx.x] = tot;
   }
 }
@@ -274,7 +279,7 @@ int fedmx_weighted_sum(const float* stack, const float* w, int K, int P, float* 
 int fedmx_param_drift(const float* hist, int M, const float* newp, const int* seg, float* out,
                       hipStream_t stream) {
   if (M <= 0) return 0;
-  hipLaunchKernelGGL(fedmx::param_drift_kernel, dim3(M), dim3(256), 0, stream, hist, newp, seg, out);
+  hipLaunchKernelGGL(fedmx::param_drift_kernel, dim3(M), dim3(1024), 0, stream, hist, newp, seg, out);
   return (int)hipGetLastError();
 }
 

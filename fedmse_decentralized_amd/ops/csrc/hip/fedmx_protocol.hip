@@ -164,9 +164,28 @@ __global__ __launch_bounds__(256) void copy_f64_kernel(double* __restrict__ dst,
   if (i < n) dst[i] = src[i];
 }
 
+// two independent copies in one launch (blockIdx.y selects the pair)
+__global__ __launch_bounds__(256) void copy2_f64_kernel(double* __restrict__ d0, const double* __restrict__ s0, int n0,
+                                                        double* __restrict__ d1, const double* __restrict__ s1,
+                                                        int n1) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.y == 0) {
+    if (i < n0) d0[i] = s0[i];
+  } else if (i < n1) {
+    d1[i] = s1[i];
+  }
+}
+
 }  // namespace fedmx
 
 extern "C" {
+
+int fedmx_copy2_f64(double* d0, const double* s0, int n0, double* d1, const double* s1, int n1, hipStream_t stream) {
+  const int n = max(n0, n1);
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(fedmx::copy2_f64_kernel, dim3((n + 255) / 256, 2), dim3(256), 0, stream, d0, s0, n0, d1, s1, n1);
+  return (int)hipGetLastError();
+}
 
 int fedmx_elect(const void* args, hipStream_t stream) {
   hipLaunchKernelGGL(fedmx::elect_kernel, dim3(1), dim3(64), 0, stream, *reinterpret_cast<const fedmx::ElectArgs*>(args));

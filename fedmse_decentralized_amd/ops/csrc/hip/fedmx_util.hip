@@ -71,50 +71,59 @@ __global__ __launch_bounds__(256) void broadcast_rows_kernel(float* __restrict__
 }
 
 // (x - mean) / (std_unbiased + 1e-8) per real column.  Rows are staged in LDS
-// in chunks of up to 256 rows (128 KB); column sums in float64.
+// in chunks of up to 256 rows (128 KB); 1024 threads = 8 row groups x 128
+// columns; column sums in float64, row groups combined in fixed order.
 constexpr int STD_CHUNK = 256;
+constexpr int STD_GROUPS = 8;
 
-__global__ __launch_bounds__(256) void standardize_lds_kernel(const float* __restrict__ x, int n, int d_in,
-                                                              float* __restrict__ y) {
+__global__ __launch_bounds__(1024) void standardize_lds_kernel(const float* __restrict__ x, int n, int d_in,
+                                                               float* __restrict__ y) {
   __shared__ __attribute__((aligned(16))) float tile[STD_CHUNK * DP];
-  __shared__ double s_part[2][DP];
+  __shared__ double s_part[STD_GROUPS][DP];
   __shared__ float s_mean[DP];
   __shared__ float s_den[DP];
   const int tid = threadIdx.x;
   const int col = tid & (DP - 1);
-  const int half = tid >> 7;  // 0/1: row parity handled by this thread
+  const int grp = tid >> 7;  // row group handled by this thread
+  const int nthr = blockDim.x;
   double sum = 0.0;
   for (int r0 = 0; r0 < n; r0 += STD_CHUNK) {
     const int rows = min(STD_CHUNK, n - r0);
-    for (int i = tid; i < rows * DP / 4; i += 256)
+    for (int i = tid; i < rows * DP / 4; i += nthr)
       reinterpret_cast<f32x4*>(tile)[i] = reinterpret_cast<const f32x4*>(x + (size_t)r0 * DP)[i];
     __syncthreads();
-    for (int r = half; r < rows; r += 2) sum += (double)tile[r * DP + col];
+    for (int r = grp; r < rows; r += STD_GROUPS) sum += (double)tile[r * DP + col];
     __syncthreads();
   }
-  s_part[half][col] = sum;
+  s_part[grp][col] = sum;
   __syncthreads();
-  const double mean = (s_part[0][col] + s_part[1][col]) / n;
+  double tot = 0.0;
+#pragma unroll
+  for (int g = 0; g < STD_GROUPS; ++g) tot += s_part[g][col];
+  const double mean = tot / n;
   __syncthreads();
   double q = 0.0;
   const bool single = (n <= STD_CHUNK);
   for (int r0 = 0; r0 < n; r0 += STD_CHUNK) {
     const int rows = min(STD_CHUNK, n - r0);
     if (!single) {
-      for (int i = tid; i < rows * DP / 4; i += 256)
+      for (int i = tid; i < rows * DP / 4; i += nthr)
         reinterpret_cast<f32x4*>(tile)[i] = reinterpret_cast<const f32x4*>(x + (size_t)r0 * DP)[i];
       __syncthreads();
     }
-    for (int r = half; r < rows; r += 2) {
+    for (int r = grp; r < rows; r += STD_GROUPS) {
       const double df = (double)tile[r * DP + col] - mean;
       q += df * df;
     }
     __syncthreads();
   }
-  s_part[half][col] = q;
+  s_part[grp][col] = q;
   __syncthreads();
-  if (half == 0) {
-    const double var = (s_part[0][col] + s_part[1][col]) / (n > 1 ? (n - 1) : 1);
+  if (grp == 0) {
+    double qq = 0.0;
+#pragma unroll
+    for (int g = 0; g < STD_GROUPS; ++g) qq += s_part[g][col];
+    const double var = qq / (n > 1 ? (n - 1) : 1);
     s_mean[col] = (float)mean;
     s_den[col] = (float)sqrt(var) + 1e-8f;
   }
@@ -122,11 +131,11 @@ __global__ __launch_bounds__(256) void standardize_lds_kernel(const float* __res
   for (int r0 = 0; r0 < n; r0 += STD_CHUNK) {
     const int rows = min(STD_CHUNK, n - r0);
     if (!single) {
-      for (int i = tid; i < rows * DP / 4; i += 256)
+      for (int i = tid; i < rows * DP / 4; i += nthr)
         reinterpret_cast<f32x4*>(tile)[i] = reinterpret_cast<const f32x4*>(x + (size_t)r0 * DP)[i];
       __syncthreads();
     }
-    for (int i = tid; i < rows * DP; i += 256) {
+    for (int i = tid; i < rows * DP; i += nthr) {
       const int cc = i & (DP - 1);
       y[(size_t)r0 * DP + i] = (cc < d_in) ? (tile[i] - s_mean[cc]) / s_den[cc] : 0.f;
     }
@@ -157,7 +166,7 @@ int fedmx_broadcast_rows(float* dst0, float* dst1, const int32_t* idx, int n, co
 
 int fedmx_standardize_lds(const float* x, int n, int d_in, float* y, hipStream_t stream) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(fedmx::standardize_lds_kernel, dim3(1), dim3(256), 0, stream, x, n, d_in, y);
+  hipLaunchKernelGGL(fedmx::standardize_lds_kernel, dim3(1), dim3(1024), 0, stream, x, n, d_in, y);
   return (int)hipGetLastError();
 }
 
