@@ -16,8 +16,7 @@ can be *enqueued* instead:
     forward(agg, every hosted client's verification data) + score_reduce
     param_drift(hist, agg)  per hosted client
     decide_adopt_kernel     ModelVerifier rule + adoption + history update
-    [RCCL all-reduce rejected counts]
-    evaluation (fwd + CEN + AUC)  [RCCL all-reduce AUCs]
+    evaluation (fwd + CEN + AUC)  [one RCCL all-reduce: rejected counts + AUCs]
     copy report vectors into a mapped per-round slot; record an event
 
 and the host moves on to the next round.  Results are *collected* later
@@ -231,8 +230,6 @@ class DeviceRound:
                                     thr=float(cfg.verification_threshold), pthr=float(cfg.performance_threshold),
                                     start=self.start, n_local=self.n_local, P=P_PAD, pad=0)
                 _hip.decide_adopt(d, dev)
-        with tel.phase("comm"):
-            comm.all_reduce_inplace(self.rej_vec)
         with tel.phase("eval"):
             eng.evaluate_launch(fed.model_type)
             aucs_ptr = eng._eval_plans[fed.model_type]["aucs_buf"].dev_ptr
@@ -243,7 +240,8 @@ class DeviceRound:
             if self.n_local:
                 _hip.copy_f64(self.metrics.data_ptr() + 8 * self.start, aucs_ptr, self.n_local, dev)
             with tel.phase("comm"):
-                comm.all_reduce_inplace(self.metrics)
+                # rejected counts and AUCs are adjacent: one RCCL all-reduce for both
+                comm.all_reduce_inplace(self.red[4 * N:])
             _hip.copy2_f64(slot_ptr, self.metrics.data_ptr(), N, slot_ptr + 8 * N, self.rej_vec.data_ptr(), N, dev)
         rec["slot"] = slot
         ev = torch.cuda.Event()

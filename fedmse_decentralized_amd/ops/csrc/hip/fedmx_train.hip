@@ -114,11 +114,11 @@ __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float 
 #endif
 }
 
-// Four elements (one accumulator register quad) at a time with packed fp32
-// math (v_pk_fma/mul/add_f32: two lanes' elements per instruction issue), the
-// transcendental sqrt/rcp per element.  Same operation order as adam_update.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
+// Four elements (one accumulator register quad) at a time, stage-major: every
+// stage issues four independent scalar ops, so consecutive VALU instructions
+// never depend on each other (no hazard s_nops between dependent packed ops,
+// which the packed-fp32 form paid on gfx950) and the scheduler can slot them
+// into MFMA gaps.  Same operation order per element as adam_update.
 template <bool PROX>
 __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4], const float (&a)[4], f32x4 g,
                                       const AdamStep& K, float& prox_acc) {
@@ -126,36 +126,39 @@ __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4
 #pragma unroll
   for (int r = 0; r < 4; ++r) adam_update<PROX>(p[r], m[r], v[r], a[r], g[r], K, prox_acc);
 #else
-  const f32x2 c1 = {K.one_m_b1, K.one_m_b1}, b2 = {K.b2, K.b2}, c2 = {K.one_m_b2, K.one_m_b2};
-  const f32x2 ib = {K.inv_bc2s, K.inv_bc2s}, ep = {K.eps, K.eps}, ns = {K.neg_step_size, K.neg_step_size};
-  f32x2 pacc = {0.f, 0.f};
+  float gr[4], t0[4], t1[4];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    f32x2 pp = {p[2 * h], p[2 * h + 1]};
-    f32x2 mm = {m[2 * h], m[2 * h + 1]};
-    f32x2 vv = {v[2 * h], v[2 * h + 1]};
-    f32x2 gg = {g[2 * h], g[2 * h + 1]};
-    if (PROX) {
-      const f32x2 aa = {a[2 * h], a[2 * h + 1]};
-      const f32x2 tm = {K.two_mu, K.two_mu};
-      const f32x2 dp = pp - aa;
-      pacc = __builtin_elementwise_fma(dp, dp, pacc);
-      gg = __builtin_elementwise_fma(tm, dp, gg);
-    }
-    mm = __builtin_elementwise_fma(c1, gg - mm, mm);
-    vv = __builtin_elementwise_fma(c2 * gg, gg, vv * b2);
-    f32x2 den = {__builtin_amdgcn_sqrtf(vv.x), __builtin_amdgcn_sqrtf(vv.y)};
-    den = __builtin_elementwise_fma(den, ib, ep);
-    const f32x2 rr = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-    pp = __builtin_elementwise_fma(ns, mm * rr, pp);
-    p[2 * h] = pp.x;
-    p[2 * h + 1] = pp.y;
-    m[2 * h] = mm.x;
-    m[2 * h + 1] = mm.y;
-    v[2 * h] = vv.x;
-    v[2 * h + 1] = vv.y;
+  for (int r = 0; r < 4; ++r) gr[r] = g[r];
+  if (PROX) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) t0[r] = p[r] - a[r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) prox_acc += t0[r] * t0[r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gr[r] = gr[r] + K.two_mu * t0[r];
   }
-  if (PROX) prox_acc += pacc.x + pacc.y;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t0[r] = gr[r] - m[r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t1[r] = K.one_m_b1 * gr[r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) m[r] = m[r] + K.one_m_b1 * t0[r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t0[r] = v[r] * K.b2;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t1[r] = (K.one_m_b2 * gr[r]) * gr[r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = t0[r] + t1[r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t0[r] = __builtin_amdgcn_sqrtf(v[r]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t0[r] = t0[r] * K.inv_bc2s + K.eps;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t1[r] = __builtin_amdgcn_rcpf(t0[r]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t1[r] = m[r] * t1[r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p[r] = p[r] + K.neg_step_size * t1[r];
 #endif
 }
 
@@ -199,15 +202,23 @@ __device__ __forceinline__ void w1_to_lds(const Slab& o, const Lane& L) {
       lds_write4(L.w1 + 16 * t * S_W1 + 16 * v, f32x4{o.q1[t][v][0], o.q1[t][v][1], o.q1[t][v][2], o.q1[t][v][3]});
 }
 
-__device__ __forceinline__ void w4own_to_lds(const Slab& o, const Lane& L) {
+__device__ __forceinline__ void w4_to_lds(const Slab& o, const Lane& L) {
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int v = 0; v < 2; ++v) L.w4[(16 * v + r) * S_W4 + 16 * t] = o.q4[v][t][r];
+}
+
+__device__ __forceinline__ void own_to_lds(const Slab& o, const Lane& L) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) L.own[r * L.own_stride] = o.o[r];
+}
+
+__device__ __forceinline__ void w4own_to_lds(const Slab& o, const Lane& L) {
+  w4_to_lds(o, L);
+  own_to_lds(o, L);
 }
 
 __device__ __forceinline__ void slab_to_lds(const Slab& o, const Lane& L) {
@@ -287,7 +298,10 @@ struct XChunk {
   f32x4 f0, f1, b0, b1;
 };
 
-template <bool PROX>
+// ONE: every batch is a single 16-row tile (batch <= 16, the reference's 12):
+// the per-chunk bookkeeping folds away and each step is one basic block the
+// scheduler can interleave (W4's optimizer VALU under the backward MFMAs).
+template <bool PROX, bool ONE>
 __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   __shared__ __attribute__((aligned(16))) float lds[L_TOTAL];
   const int w = threadIdx.x >> 6;
@@ -570,9 +584,9 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
     while (bi < nb) {
       const int row_b = bi * B;
       const int bt = min(B, n_tr - row_b);
-      const int nch = (bt + 15) >> 4;
-      const int bc = min(16, bt - 16 * ch);
-      const bool last = (ch == nch - 1);
+      const int nch = ONE ? 1 : (bt + 15) >> 4;
+      const int bc = ONE ? bt : min(16, bt - 16 * ch);
+      const bool last = ONE || (ch == nch - 1);
       // next chunk position
       const int bi_n = last ? bi + 1 : bi;
       const int ch_n = last ? 0 : ch + 1;
@@ -679,6 +693,25 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         }
         dh3[t] = s;
       }
+      float prox_acc = 0.f;  // sum (p - anchor)^2 of owned params (pre-update)
+      if (last) {
+        ++step;
+        b1pow *= (double)A.beta1;
+        b2pow *= (double)A.beta2;
+        K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
+        K.bc2s = (float)sqrt(1.0 - b2pow);
+        K.inv_bc2s = 1.0f / K.bc2s;
+        // W4 is not read again this step (its dH3 product ran before barrier
+        // #2): update it here, where its VALU work overlaps the backward MFMAs
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) adam4<PROX>(P.q4[v][t], M.q4[v][t], V.q4[v][t], AN.q4[v][t], G4[v][t], K, prox_acc);
+        // publish the own W4 rows now (read back by this wave only, by the
+        // next layer-4 product): the stores pin the update ahead of the
+        // wave_sync below instead of letting it sink to the step's end
+        w4_to_lds(P, L);
+      }
       if (w < 2) {  // dH3^T for the owned dW3 tile (dY^T reads are done)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
@@ -740,13 +773,6 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       }
       STAMP(stamp_on, 9);
       if (last) {
-        ++step;
-        b1pow *= (double)A.beta1;
-        b2pow *= (double)A.beta2;
-        K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
-        K.bc2s = (float)sqrt(1.0 - b2pow);
-        K.inv_bc2s = 1.0f / K.bc2s;
-        float prox_acc = 0.f;  // sum (p - anchor)^2 of owned params (pre-update)
         // W1 first: the next chunk's layer-1 product waits on it
 #pragma unroll
         for (int t = 0; t < 2; ++t)
@@ -757,14 +783,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
           finalize_chunk(bc_n, nxt);
           l1_partial(nxt, l1a, l1b);
         }
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-#pragma unroll
-          for (int t = 0; t < 2; ++t) adam4<PROX>(P.q4[v][t], M.q4[v][t], V.q4[v][t], AN.q4[v][t], G4[v][t], K, prox_acc);
         adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
         if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
-        // publish own W4 rows (read back by this wave only) and the owned small tile
-        w4own_to_lds(P, L);
+        // publish the owned small tile (read by every wave after barrier #1)
+        own_to_lds(P, L);
       } else {
         finalize_chunk(bc_n, nxt);
         l1_partial(nxt, l1a, l1b);
@@ -887,10 +909,18 @@ int fedmx_train(const void* args, int k, hipStream_t stream) {
   if (A.d_in < 1 || A.d_in > fedmx::DP - 1 || A.hidden < 1 || A.hidden > fedmx::HP - 1 || A.latent < 1 ||
       A.latent > fedmx::ZP - 1)
     return -3;
-  if (A.mu != 0.f)
-    hipLaunchKernelGGL(fedmx::train_kernel<true>, dim3(k), dim3(256), 0, stream, A);
-  else
-    hipLaunchKernelGGL(fedmx::train_kernel<false>, dim3(k), dim3(256), 0, stream, A);
+  const bool one = A.batch <= 16;
+  if (A.mu != 0.f) {
+    if (one)
+      hipLaunchKernelGGL((fedmx::train_kernel<true, true>), dim3(k), dim3(256), 0, stream, A);
+    else
+      hipLaunchKernelGGL((fedmx::train_kernel<true, false>), dim3(k), dim3(256), 0, stream, A);
+  } else {
+    if (one)
+      hipLaunchKernelGGL((fedmx::train_kernel<false, true>), dim3(k), dim3(256), 0, stream, A);
+    else
+      hipLaunchKernelGGL((fedmx::train_kernel<false, false>), dim3(k), dim3(256), 0, stream, A);
+  }
   return (int)hipGetLastError();
 }
 
