@@ -28,6 +28,10 @@ import torch
 from . import _hiprt, build
 
 _lock = threading.Lock()
+# 4: one wave per SIMD (default, fastest measured); 8: two waves per SIMD
+# (fedmx_train8.hip, batch <= 16) — 1.62 ms vs 1.39 ms per 5-client x 5-epoch
+# launch on MI355X (profiles/r1_train8_stamps.txt)
+TRAIN_WAVES = int(os.environ.get("FEDMX_TRAIN_WAVES", "4"))
 _lib = None
 
 FWD_DTYPE = np.dtype([
@@ -106,6 +110,7 @@ def lib():
                 "fedmx_score_reduce": [vp, i32, i32, vp],
                 "fedmx_broadcast_rows": [vp, vp, vp, i32, vp, i32, vp],
                 "fedmx_train": [ctypes.POINTER(TrainArgs), i32, vp],
+                "fedmx_train8": [ctypes.POINTER(TrainArgs), i32, vp],
                 "fedmx_probe_mfma": [vp, vp],
                 "fedmx_elect": [ctypes.POINTER(ElectArgs), vp],
                 "fedmx_gather_wsum": [ctypes.POINTER(WsumArgs), vp],
@@ -432,7 +437,7 @@ class TrainBuffers:
         self.valid_off = torch.from_numpy(store.valid_off).to(dev)
 
 
-def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tensor] = None):
+def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tensor] = None, waves: int = 0):
     """Launch the fused training kernel for store rows ``local_ids`` (async).
     Returns host views (tracking[k, E, 2], epochs_run[k], best_epoch[k])
     written by the kernel, valid after the next stream sync."""
@@ -469,7 +474,11 @@ def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tens
     a.lr, a.beta1, a.beta2, a.eps = hp.lr, hp.beta1, hp.beta2, hp.eps
     a.lam, a.mu = hp.shrink_lambda, hp.fedprox_mu
     a.stamps = stamps.data_ptr() if stamps is not None else None
-    rc = lib().fedmx_train(ctypes.byref(a), k, rt.stream)
+    # the 8-wave variant covers single-tile batches only
+    if hp.batch_size <= 16 and (waves or TRAIN_WAVES) == 8:
+        rc = lib().fedmx_train8(ctypes.byref(a), k, rt.stream)
+    else:
+        rc = lib().fedmx_train(ctypes.byref(a), k, rt.stream)
     if rc == -2:
         raise ValueError(f"fused training kernel needs batch_size >= 1, got {hp.batch_size}")
     _check(rc, "fedmx_train")

@@ -49,7 +49,8 @@ def main():
     eng.setup([c.train for c in clients], [c.valid for c in clients], [c.test for c in clients],
               [c.test_label for c in clients], init)
     hp = TrainHParams(epochs=5, batch_size=12, lr=1e-3, shrink_lambda=5.0, patience=10 ** 6)
-    stamps = torch.zeros(4 * 32, dtype=torch.int64, device=dev)
+    stamps = torch.zeros(8 * 32, dtype=torch.int64, device=dev)
+    nw = 8 if (_hip.TRAIN_WAVES == 8) else 4
     if PLAIN:
         for _ in range(3):
             _hip.train(eng.store, list(range(5)), hp, eng.dims)
@@ -60,10 +61,10 @@ def main():
     for rep in range(3):
         _hip.train(eng.store, list(range(5)), hp, eng.dims, stamps=stamps)
         torch.cuda.synchronize()
-        st = stamps.view(4, 32).cpu().numpy().astype(np.int64)
+        st = stamps.view(8, 32).cpu().numpy().astype(np.int64)[:nw]
         res = {}
         for a, b, name in PHASES:
-            res[name] = [int(st[w, b] - st[w, a]) if st[w, a] and st[w, b] else None for w in range(4)]
+            res[name] = [int(st[w, b] - st[w, a]) if st[w, a] and st[w, b] else None for w in range(nw)]
         out[f"rep{rep}"] = res
         stamps.zero_()
     for name, v in out["rep2"].items():
