@@ -16,8 +16,11 @@ can be *enqueued* instead:
     forward(agg, every hosted client's verification data) + score_reduce
     param_drift(hist, agg)  per hosted client
     decide_adopt_kernel     ModelVerifier rule + adoption + history update
-    evaluation (fwd + CEN + AUC)  [one RCCL all-reduce: rejected counts + AUCs]
-    copy report vectors into a mapped per-round slot; record an event
+    [RCCL all-reduce rejected counts] -> mapped per-round report slot
+    side stream: snapshot params / best, evaluation (fwd + CEN + AUC)
+                 [RCCL all-reduce AUCs] -> report slot; record the round event
+                 (overlaps the next round's training, which waits only for
+                 the snapshot copies)
 
 and the host moves on to the next round.  Results are *collected* later
 (at most ``max_pending`` rounds behind, or when a caller reads a round's
@@ -105,10 +108,16 @@ class DeviceRound:
         f64, i32, f32 = torch.float64, torch.int32, torch.float32
         # one buffer for the per-round report vectors: a single fill per round
         # when ranks sum them (single rank: every entry read is rewritten each round)
-        self.red = torch.zeros(6 * N, dtype=f64, device=dev)
+        self.red = torch.zeros(5 * N, dtype=f64, device=dev)
         self.vec = self.red[:4 * N].view(N, 4)
         self.rej_vec = self.red[4 * N:5 * N]
-        self.metrics = self.red[5 * N:]
+        # evaluation runs on a side stream and overlaps the next round's
+        # training: it reads a snapshot of the parameters taken right after
+        # the adoption step, into its own metrics buffer
+        self.side = torch.cuda.Stream(device=dev)
+        self.metrics = torch.zeros(N, dtype=f64, device=dev)
+        self.eval_params = torch.empty_like(st.params)
+        self._ev_copy = None
         self.agg_counts = torch.zeros(N, dtype=i32, device=dev)
         self.weights = torch.zeros(max(N, 1), dtype=f32, device=dev)
         self.state = torch.full((4,), -1, dtype=i32, device=dev)
@@ -157,12 +166,10 @@ class DeviceRound:
         rec = dict(round=rnd, selected=list(selected), local_sel=local_sel, done=False)
 
         with tel.phase("train"):
+            if self._ev_copy is not None:   # the previous round's eval / snapshot copies have read params / best
+                torch.cuda.current_stream(dev).wait_event(self._ev_copy)
             handle = eng.train_launch(local_rows, fed.hp) if local_sel else None
             rec["handle"] = handle
-            if local_sel and cfg.save_checkpoints:
-                from ..io.async_writer import snapshot_to_host
-
-                rec["snap"] = snapshot_to_host(st.best)
         with tel.phase("vote"):
             if comm.world_size > 1:
                 self.red.zero_()
@@ -230,22 +237,34 @@ class DeviceRound:
                                     thr=float(cfg.verification_threshold), pthr=float(cfg.performance_threshold),
                                     start=self.start, n_local=self.n_local, P=P_PAD, pad=0)
                 _hip.decide_adopt(d, dev)
-        with tel.phase("eval"):
-            eng.evaluate_launch(fed.model_type)
-            aucs_ptr = eng._eval_plans[fed.model_type]["aucs_buf"].dev_ptr
         slot_ptr, slot = self.rt.out.take(np.float64, 2 * N)
-        if comm.world_size == 1:
-            _hip.copy2_f64(slot_ptr, aucs_ptr, N, slot_ptr + 8 * N, self.rej_vec.data_ptr(), N, dev)
-        else:
-            if self.n_local:
-                _hip.copy_f64(self.metrics.data_ptr() + 8 * self.start, aucs_ptr, self.n_local, dev)
-            with tel.phase("comm"):
-                # rejected counts and AUCs are adjacent: one RCCL all-reduce for both
-                comm.all_reduce_inplace(self.red[4 * N:])
-            _hip.copy2_f64(slot_ptr, self.metrics.data_ptr(), N, slot_ptr + 8 * N, self.rej_vec.data_ptr(), N, dev)
+        with tel.phase("comm"):
+            comm.all_reduce_inplace(self.rej_vec)
+        _hip.copy_f64(slot_ptr + 8 * N, self.rej_vec.data_ptr(), N, dev)
+        ev_dec = torch.cuda.Event()
+        ev_dec.record()
+        with tel.phase("eval"), _hip.on_stream(self.side):
+            self.side.wait_event(ev_dec)
+            self.eval_params.copy_(st.params)
+            if local_sel and cfg.save_checkpoints:
+                from ..io.async_writer import snapshot_to_host
+
+                rec["snap"] = snapshot_to_host(st.best)
+            self._ev_copy = torch.cuda.Event()
+            self._ev_copy.record(self.side)
+            eng.evaluate_launch(fed.model_type, params=self.eval_params)
+            aucs_ptr = eng._plan(fed.model_type, self.eval_params)["aucs_buf"].dev_ptr
+            if comm.world_size == 1:
+                _hip.copy_f64(slot_ptr, aucs_ptr, N, dev)
+            else:
+                self.metrics.zero_()
+                if self.n_local:
+                    _hip.copy_f64(self.metrics.data_ptr() + 8 * self.start, aucs_ptr, self.n_local, dev)
+                comm.all_reduce_inplace(self.metrics)
+                _hip.copy_f64(slot_ptr, self.metrics.data_ptr(), N, dev)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
         rec["slot"] = slot
-        ev = torch.cuda.Event()
-        ev.record()
         rec["event"] = ev
         fed.round_idx += 1
         rec["times_ms"] = tel.end_round(round=rnd + 1, selected=k, aggregator=None)

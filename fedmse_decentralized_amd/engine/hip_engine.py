@@ -152,8 +152,12 @@ class HipEngine(Engine):
         st = self.store
         _hip.broadcast_rows(st.params, st.anchor if anchor else None, list(local_rows), agg)
 
-    def _plan(self, model_type: str) -> dict:
-        p = self._eval_plans.get(model_type)
+    def _plan(self, model_type: str, params: Optional[torch.Tensor] = None) -> dict:
+        """Cached evaluation launch plan; ``params`` (default: the live client
+        parameters) is the [C, P] buffer the forward reads."""
+        params = self.store.params if params is None else params
+        key = (model_type, params.data_ptr())
+        p = self._eval_plans.get(key)
         if p is not None:
             return p
         st = self.store
@@ -165,7 +169,7 @@ class HipEngine(Engine):
             items = []
             for c in range(C):
                 items += [(c, st.rows("train", c)), (c, st.rows("test", c))]
-            fwd = _hip.FwdPlan(st.params, items, self.dims, want_sse=False, want_latent=True)
+            fwd = _hip.FwdPlan(params, items, self.dims, want_sse=False, want_latent=True)
             lat = fwd.lat_views()
             scores_all = torch.empty(sum(int(st.test_off[c + 1] - st.test_off[c]) for c in range(C)),
                                      dtype=torch.float64, device=self.device)
@@ -174,7 +178,7 @@ class HipEngine(Engine):
             adesc = _hip.auc_desc(scores, labels, aucs_buf.dev_ptr, 1.0)
             p = dict(fwd=fwd, cen=cdesc_dev, ncen=C, scores=scores, test_lat=lat[1::2])
         elif model_type == "autoencoder":
-            fwd = _hip.FwdPlan(st.params, [(c, st.rows("test", c)) for c in range(C)], self.dims,
+            fwd = _hip.FwdPlan(params, [(c, st.rows("test", c)) for c in range(C)], self.dims,
                                want_sse=True, want_latent=False)
             scores = fwd.sse_views()
             adesc = _hip.auc_desc(scores, labels, aucs_buf.dev_ptr, 1.0 / self.dims.d_in)
@@ -185,13 +189,13 @@ class HipEngine(Engine):
         p["aucs"] = aucs
         p["aucs_buf"] = aucs_buf
         p["labels"] = labels
-        self._eval_plans[model_type] = p
+        self._eval_plans[key] = p
         return p
 
-    def evaluate_launch(self, model_type: str) -> np.ndarray:
+    def evaluate_launch(self, model_type: str, params: Optional[torch.Tensor] = None) -> np.ndarray:
         """Enqueue the full AUC evaluation of every hosted client; returns the
         host view of the AUCs (float64 [C], valid after the next sync)."""
-        p = self._plan(model_type)
+        p = self._plan(model_type, params)
         p["fwd"].run()
         if p["cen"] is not None:
             _hip.launch_cen(p["cen"], p["ncen"], self.device)
@@ -204,7 +208,7 @@ class HipEngine(Engine):
         if metric != "AUC":
             return evaluate_clients(self, list(range(self.store.num_clients)), model_type, metric, keep_latents)
         aucs = self.evaluate_launch(model_type)
-        p = self._eval_plans[model_type]
+        p = self._plan(model_type)
         vals = self._auc_fixup(self.fetch([aucs])[0], p["scores"], p["labels"])
         latents = None
         if keep_latents and p["test_lat"] is not None:

@@ -164,8 +164,34 @@ def runtime(device: torch.device) -> Runtime:
     return r
 
 
+_tls = threading.local()
+
+
 def _stream(device: torch.device) -> int:
-    return runtime(device).stream
+    s = getattr(_tls, "stream", None)
+    return s if s is not None else runtime(device).stream
+
+
+class on_stream:
+    """Route the cached-plan launches (FwdPlan.run, launch_cen / launch_auc /
+    launch_score_reduce, copy kernels) to another HIP stream (a
+    ``torch.cuda.Stream``), e.g. evaluation overlapping the next round's
+    training; torch work inside the block follows the same stream."""
+
+    def __init__(self, stream: "torch.cuda.Stream"):
+        self.stream = stream
+        self._ctx = torch.cuda.stream(stream)
+
+    def __enter__(self):
+        self._prev = getattr(_tls, "stream", None)
+        _tls.stream = self.stream.cuda_stream
+        self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        self._ctx.__exit__(*exc)
+        _tls.stream = self._prev
+        return False
 
 
 # ---------------------------------------------------------------------------

@@ -55,6 +55,8 @@ def rt():
                 L.hipStreamSynchronize.restype = ctypes.c_int
                 L.hipHostFree.argtypes = [vp]
                 L.hipHostFree.restype = ctypes.c_int
+                L.hipDeviceSynchronize.argtypes = []
+                L.hipDeviceSynchronize.restype = ctypes.c_int
                 _lib = L
     return _lib
 
@@ -63,6 +65,13 @@ def stream_sync(stream: int) -> None:
     rc = rt().hipStreamSynchronize(ctypes.c_void_p(stream))
     if rc != 0:
         raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
+    SyncClock.tick()
+
+
+def device_sync() -> None:
+    rc = rt().hipDeviceSynchronize()
+    if rc != 0:
+        raise RuntimeError(f"hipDeviceSynchronize failed ({rc})")
     SyncClock.tick()
 
 
@@ -122,7 +131,7 @@ class _Ring:
             # wrapping: earlier regions may still be read/written by queued kernels
             # unless a stream synchronisation happened since this pass began
             if SyncClock.gen <= self.wrap_gen:
-                stream_sync(self.stream)
+                device_sync()   # kernels on any stream may still read the ring
             self.off = 0
             self.wrap_gen = SyncClock.gen
         o = self.off
