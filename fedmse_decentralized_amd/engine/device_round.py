@@ -7,7 +7,7 @@ training + voting, after verification, after evaluation).  With
 a host RNG whose consumption does not depend on results, so the whole round
 can be *enqueued* instead:
 
-    train (fused kernel, all local selected clients)     -> best snapshot D2H (async)
+    train (fused kernel, all local selected clients)
     zero report vectors; standardise vote data; forward + score_reduce -> vec[N,4]
     [RCCL all-reduce vec]                                 (vote scores, dev MSEs)
     elect_kernel            aggregator, cap counts, FedAvg / FedMSE weights
@@ -17,7 +17,8 @@ can be *enqueued* instead:
     param_drift(hist, agg)  per hosted client
     decide_adopt_kernel     ModelVerifier rule + adoption + history update
     [RCCL all-reduce rejected counts] -> mapped per-round report slot
-    side stream: snapshot params / best, evaluation (fwd + CEN + AUC)
+    snapshot params / best models (one fused device copy)
+    side stream: best models -> mapped host snapshot slot, evaluation (fwd + CEN + AUC)
                  [RCCL all-reduce AUCs] -> report slot; record the round event
                  (overlaps the next round's training, which waits only for
                  the snapshot copies)
@@ -36,6 +37,7 @@ per round in both paths.
 from __future__ import annotations
 
 import logging
+import threading
 from collections import deque
 from typing import Dict, List, Optional
 
@@ -117,7 +119,22 @@ class DeviceRound:
         self.side = torch.cuda.Stream(device=dev)
         self.metrics = torch.zeros(N, dtype=f64, device=dev)
         self.eval_params = torch.empty_like(st.params)
-        self._ev_copy = None
+        self.best_stage = torch.empty_like(st.best)
+        self._ev_side_done = None
+        # best-model snapshots for the artefact writer: a ring of mapped host
+        # slots filled by a device copy kernel (no torch pinned allocation or
+        # blocking copy on the enqueue path); a slot is reused once the writer
+        # has finished the checkpoint jobs that read it
+        self.n_snap = 4
+        numel = st.best.numel()
+        self.snap_buf = _hip._hiprt.MappedBuffer(self.n_snap * numel * 4)
+        C = st.best.shape[0]
+        self.snap_views = [torch.from_numpy(self.snap_buf.view(i * numel * 4, np.float32, numel).reshape(C, -1))
+                           for i in range(self.n_snap)]
+        self.snap_free = [threading.Event() for _ in range(self.n_snap)]
+        for e in self.snap_free:
+            e.set()
+        self.snap_i = 0
         self.agg_counts = torch.zeros(N, dtype=i32, device=dev)
         self.weights = torch.zeros(max(N, 1), dtype=f32, device=dev)
         self.state = torch.full((4,), -1, dtype=i32, device=dev)
@@ -166,8 +183,6 @@ class DeviceRound:
         rec = dict(round=rnd, selected=list(selected), local_sel=local_sel, done=False)
 
         with tel.phase("train"):
-            if self._ev_copy is not None:   # the previous round's eval / snapshot copies have read params / best
-                torch.cuda.current_stream(dev).wait_event(self._ev_copy)
             handle = eng.train_launch(local_rows, fed.hp) if local_sel else None
             rec["handle"] = handle
         with tel.phase("vote"):
@@ -241,17 +256,27 @@ class DeviceRound:
         with tel.phase("comm"):
             comm.all_reduce_inplace(self.rej_vec)
         _hip.copy_f64(slot_ptr + 8 * N, self.rej_vec.data_ptr(), N, dev)
+        # snapshot params (for the evaluation) and the best models (for the
+        # artefacts) on the main stream: one fused device copy, so the next
+        # round's training can start right away
+        if self._ev_side_done is not None:   # the previous round's side work has read the snapshots
+            torch.cuda.current_stream(dev).wait_event(self._ev_side_done)
+        nd = st.params.numel() // 2
+        _hip.copy2_f64(self.eval_params.data_ptr(), st.params.data_ptr(), nd,
+                       self.best_stage.data_ptr(), st.best.data_ptr(), nd, dev)
         ev_dec = torch.cuda.Event()
         ev_dec.record()
         with tel.phase("eval"), _hip.on_stream(self.side):
             self.side.wait_event(ev_dec)
-            self.eval_params.copy_(st.params)
             if local_sel and cfg.save_checkpoints:
-                from ..io.async_writer import snapshot_to_host
-
-                rec["snap"] = snapshot_to_host(st.best)
-            self._ev_copy = torch.cuda.Event()
-            self._ev_copy.record(self.side)
+                si = self.snap_i
+                self.snap_i = (si + 1) % self.n_snap
+                self.snap_free[si].wait()
+                self.snap_free[si].clear()
+                nd = st.best.numel() // 2
+                _hip.copy2_f64(self.snap_buf.dev_ptr + si * st.best.numel() * 4, self.best_stage.data_ptr(), nd,
+                               0, 0, 0, dev)
+                rec["snap_slot"] = si
             eng.evaluate_launch(fed.model_type, params=self.eval_params)
             aucs_ptr = eng._plan(fed.model_type, self.eval_params)["aucs_buf"].dev_ptr
             if comm.world_size == 1:
@@ -264,6 +289,7 @@ class DeviceRound:
                 _hip.copy_f64(slot_ptr, self.metrics.data_ptr(), N, dev)
             ev = torch.cuda.Event()
             ev.record(self.side)
+            self._ev_side_done = ev
         rec["slot"] = slot
         rec["event"] = ev
         fed.round_idx += 1
@@ -312,8 +338,9 @@ class DeviceRound:
                     for e, (tl, vl) in enumerate(res.tracking[i]):
                         log.info(f"[Client {c}] Epoch {e + 1} - Training loss: {tl} - Validating loss: {vl}")
             if cfg.save_checkpoints:
-                snap, ev = rec["snap"]
-                fed._submit_checkpoints(res, rec["local_sel"], snap, ev)
+                si = rec["snap_slot"]
+                fed._submit_checkpoints(res, rec["local_sel"], self.snap_views[si], None)
+                fed.writer.submit(self.snap_free[si].set)
         verification = []
         if aggregator is not None:
             self.host_agg_counts[aggregator] += 1
@@ -341,6 +368,6 @@ class DeviceRound:
             stop = fed.early.update(float(np.min(metrics)))
         rec.update(aggregator=aggregator, metrics=metrics, verification=verification, epochs_run=epochs_local,
                    stop=stop, done=True)
-        for key in ("handle", "snap", "slot", "report", "_keep", "event"):
+        for key in ("handle", "snap_slot", "slot", "report", "_keep", "event"):
             rec.pop(key, None)
         self.all_rounds.pop(rnd, None)
