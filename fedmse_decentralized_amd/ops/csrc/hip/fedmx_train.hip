@@ -40,6 +40,10 @@
 // columns and padded features are masked out of the loss and every gradient.
 #include "fedmx_train_common.h"
 
+#ifndef FEDMX_SCHED_HINTS
+#define FEDMX_SCHED_HINTS 1
+#endif
+
 namespace fedmx {
 
 // LDS plan (floats); total < 160 KiB -> one workgroup per CU.
@@ -548,12 +552,12 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         // wave_sync below instead of letting it sink to the step's end
         w4_to_lds(P, L);
       }
-      if (w < 2) {  // dH3^T for the owned dW3 tile (dY^T reads are done)
+      // dH3^T for the owned dW3 tile (dY^T reads are done).  Written by every
+      // wave (own scratch) so the step stays one basic block for the scheduler.
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) sT0[tw + (16 * t + r) * S_T] = dh3[t][r];
-      }
+        for (int r = 0; r < 4; ++r) sT0[tw + (16 * t + r) * S_T] = dh3[t][r];
       // ---- dZ = W3a^T dH3 (pre-update W3, every wave), + shrink-loss gradient
       //      lambda/B * z / ||z|| (0 where ||z|| == 0)
       f32x4 dz = zero4();
@@ -565,10 +569,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       const float shr = (c < bc && norm_c > 0.f) ? shr_raw : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) dz[r] = (4 * g + r < latent) ? dz[r] + shr * z[r] : 0.f;
-      if (w >= 2) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sDZT[tw + r * S_T] = dz[r];
-      }
+      for (int r = 0; r < 4; ++r) sDZT[tw + r * S_T] = dz[r];
       // ---- dH1 in the batch-major layout, D[b=4g+r][h=16t+c] = sum_z dZ[b][z] W2a[z][h]
       //      (A = dZ^T D tile as is, B = W2a D layout), ReLU mask from H1^T
       //      read in the same layout; this is directly dW1's B operand.
@@ -596,14 +598,9 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       // ---- owned small tile: w<2 -> dW3 tile (h-block w) = dH3^T Z ;
       //                        w>=2 -> dW2 tile (h-block w-2) = dZ^T H1
       {
-        f32x4 a, b;
-        if (w < 2) {
-          a = lds_read4(sT0 + tr + 16 * w * S_T);
-          b = lds_read4(sZT + tr);
-        } else {
-          a = lds_read4(sDZT + tr);
-          b = (w == 2) ? h1b[0] : h1b[1];
-        }
+        const f32x4 a = lds_read4(w < 2 ? sT0 + tr + 16 * w * S_T : sDZT + tr);
+        const f32x4 bz = lds_read4(sZT + tr);
+        const f32x4 b = (w < 2) ? bz : ((w == 2) ? h1b[0] : h1b[1]);
 #pragma unroll
         for (int s = 0; s < 4; ++s) Go = mfma16(a[s], b[s], Go);
       }
@@ -615,14 +612,27 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
 #pragma unroll
           for (int v = 0; v < 2; ++v) adam4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
         STAMP(stamp_on, 10);
-        if (has_next) {
-          finalize_chunk(bc_n, nxt);
-          l1_partial(nxt, l1a, l1b);
-        }
+        // (after an epoch's last batch this works on a stale tile; the result
+        // is unused and the product stays branch-free)
+        finalize_chunk(bc_n, nxt);
+        l1_partial(nxt, l1a, l1b);
         adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
         if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
         // publish the owned small tile (read by every wave after barrier #1)
         own_to_lds(P, L);
+#if FEDMX_SCHED_HINTS
+        if (ONE) {
+          // Everything from barrier #2 to here is one basic block (ONE): ask
+          // the scheduler to interleave the optimizer / mask VALU work into
+          // the MFMA gaps (one wave per SIMD co-issues ~6 VALU per 16x16x4
+          // MFMA) instead of running the two streams back to back.
+#pragma unroll
+          for (int i = 0; i < 64; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // 6 VALU
+          }
+        }
+#endif
       } else {
         finalize_chunk(bc_n, nxt);
         l1_partial(nxt, l1a, l1b);
