@@ -100,6 +100,9 @@ class ExperimentConfig:
     # fixed compat + HIP engine: run the round's protocol decisions on the
     # device (engine/device_round.py) so rounds need no host synchronisation
     device_protocol: bool = True
+    # debug: all-gather a hash of the replicated protocol state every round
+    # and fail on divergence between ranks
+    debug_replica_check: bool = False
 
     # -----------------------------------------------------------------------
     @property

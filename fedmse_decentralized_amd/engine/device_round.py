@@ -363,6 +363,8 @@ class DeviceRound:
             m_ = metrics.copy()
             fed.writer.submit(lambda m_=m_, rnd=rnd: fed._report_round(rnd, m_))
         fed.last_metrics = metrics
+        if cfg.debug_replica_check:
+            fed.check_replicas(rnd, rec["selected"], aggregator, metrics)
         stop = False
         if cfg.global_early_stop:
             stop = fed.early.update(float(np.min(metrics)))

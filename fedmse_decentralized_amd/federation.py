@@ -221,6 +221,18 @@ class Federation:
         if getattr(self, "_fast", None) is not None:
             self._fast.collect_all()
 
+    def check_replicas(self, rnd: int, selected, aggregator, metrics) -> None:
+        """Fail loudly if the replicated protocol state differs between ranks."""
+        import hashlib
+
+        h = hashlib.sha256()
+        h.update(repr((rnd, list(selected), aggregator, list(self.agg_counts))).encode())
+        h.update(np.ascontiguousarray(metrics, dtype=np.float64).tobytes())
+        digest = h.hexdigest()
+        allh = self.comm.all_gather_object(digest)
+        if len(set(allh)) != 1:
+            raise RuntimeError(f"replicated protocol state diverged at round {rnd + 1}: {allh}")
+
     # -- report / artefact submission (background writer) ---------------------------
     def _report_round(self, rnd: int, metrics: np.ndarray) -> None:
         reports.append_round_result(self.cfg, self.run, rnd, metrics, self.model_type, self.update_type)
@@ -429,6 +441,8 @@ class Federation:
             m_ = metrics.copy()
             self.writer.submit(lambda m_=m_, rnd=rnd: self._report_round(rnd, m_))
         self.last_metrics = metrics
+        if cfg.debug_replica_check:
+            self.check_replicas(rnd, selected, aggregator, metrics)
         stop = False
         if cfg.global_early_stop:
             stop = self.early.update(float(np.min(metrics)))

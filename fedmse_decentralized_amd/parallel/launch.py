@@ -36,7 +36,8 @@ def init_comm(backend: Optional[str] = None, device: Optional[str] = None, timeo
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if backend is None:
-        backend = "nccl" if device == "cuda" else "gloo"
+        # FEDMX_DIST_BACKEND=gloo: multi-rank rehearsal on one GPU (RCCL needs distinct GPUs)
+        backend = os.environ.get("FEDMX_DIST_BACKEND") or ("nccl" if device == "cuda" else "gloo")
     if device == "cuda":
         # FEDMX_DEVICE_INDEX pins every rank to one GPU (multi-rank tests on a
         # one-GPU box, with the gloo backend; RCCL needs distinct GPUs)

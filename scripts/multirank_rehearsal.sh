@@ -1,0 +1,22 @@
+#!/bin/bash
+# Multi-rank rehearsal of bench.py / main.py on a ONE-GPU box: 2 ranks share
+# cuda:0 over the gloo backend (RCCL refuses duplicate GPUs).  Exercises the
+# sharded federation, the device-resident protocol's collectives and the
+# bench JSON contract (max over ranks) end to end.
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export FEDMX_DEVICE_INDEX=0 FEDMX_DIST_BACKEND=gloo HSA_ENABLE_IPC_MODE_LEGACY=0
+python -c "import fedmse_decentralized_amd.ops.build as b; b.build_all()" || exit 3
+timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 > "$OUT/rehearsal_bench2.log" 2>&1
+rc=$?
+echo "bench 2 ranks rc=$rc"; tail -n 3 "$OUT/rehearsal_bench2.log"
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29518 main.py --synthetic nbaiot --num-rounds 2 --epoch 1 --model-types hybrid \
+  --update-types mse_avg --compat fixed --output-root "$OUT/rehearsal_main" --log-level WARNING > "$OUT/rehearsal_main2.log" 2>&1
+rc=$?
+echo "main 2 ranks rc=$rc"; tail -n 3 "$OUT/rehearsal_main2.log"
+exit $rc

@@ -110,7 +110,8 @@ def _worker(rank, world, port, out):
     from fedmse_decentralized_amd.parallel.launch import init_comm, shutdown
 
     comm = init_comm(backend="gloo", device="cuda")
-    fed, res = _run(_cfg(os.path.join(out, f"r{rank}"), save_checkpoints=False), "mse_avg", 4, comm=comm)
+    fed, res = _run(_cfg(os.path.join(out, f"r{rank}"), save_checkpoints=False, debug_replica_check=True), "mse_avg",
+                    4, comm=comm)
     res["fast"] = fed._fast is not None
     res["params"] = fed.engine.store.params.double().sum(1).tolist()
     res["local"] = fed.local
@@ -134,3 +135,14 @@ def test_device_round_two_ranks_one_gpu(tmp_path):
             np.testing.assert_array_equal(np.array(x), np.array(y))
         loc = d["local"]
         assert d["params"] == ref_params[loc[0]:loc[-1] + 1]
+
+
+def test_device_round_is_deterministic(tmp_path):
+    """Run-to-run determinism: two identical device-protocol
+    runs give bit-identical parameters, Adam state and metrics."""
+    _shrink()
+    fa, a = _run(_cfg(str(tmp_path / "a"), save_checkpoints=False), "mse_avg", 4)
+    fb, b = _run(_cfg(str(tmp_path / "b"), save_checkpoints=False), "mse_avg", 4)
+    assert a == b
+    for name in ("params", "adam_m", "adam_v", "anchor", "best"):
+        assert torch.equal(getattr(fa.engine.store, name), getattr(fb.engine.store, name)), name

@@ -191,3 +191,25 @@ def test_csv_config_path_end_to_end(tmp_path):
     assert len(fed.clients) == 3
     r = fed.run_round()
     assert r.metrics.shape == (3,) and np.all((r.metrics >= 0) & (r.metrics <= 1))
+
+
+def test_replica_check_passes_and_detects_divergence(tmp_path):
+    cfg = _cfg(tmp_path, global_early_stop=False, save_checkpoints=False, network_size=4, debug_replica_check=True)
+    outs = _run_threads(2, cfg, 2)          # identical replicas: the check passes every round
+    assert outs[0][0].aggregator == outs[1][0].aggregator
+    fed = Federation(cfg, "hybrid", "avg", 0).setup()
+    comms = ThreadComm.group(2)
+    errs = []
+
+    def worker(r):
+        f = Federation(cfg, "hybrid", "avg", 0, comm=comms[r], device=torch.device("cpu")).setup()
+        try:
+            f.check_replicas(0, [0, 1], r, np.zeros(4))   # rank-dependent aggregator
+        except RuntimeError as e:
+            errs.append(str(e))
+    ts = [threading.Thread(target=worker, args=(r,)) for r in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert len(errs) == 2 and "diverged" in errs[0]
