@@ -54,6 +54,9 @@ def main(argv=None):
     p.add_argument("--model-type", default="hybrid")
     p.add_argument("--update-type", default="mse_avg")
     p.add_argument("--backend", default="auto")
+    p.add_argument("--data-kind", default="nbaiot", choices=["nbaiot", "kitsune"],
+                   help="synthetic feature family (BASELINE config 5 uses kitsune, non-IID)")
+    p.add_argument("--non-iid", action="store_true", help="Dirichlet non-IID client mixtures")
     p.add_argument("--compat", default="fixed")
     p.add_argument("--no-artifacts", action="store_true", help="skip model.cpt/tracking/JSONL writes")
     p.add_argument("--trace", default=None, help="per-phase JSONL trace (adds device syncs)")
@@ -78,7 +81,7 @@ def main(argv=None):
         num_participants=0.5, epoch=args.epochs, num_rounds=10 ** 9, lr_rate=1e-3, shrink_lambda=5,
         network_size=args.clients_per_gpu * n_gpus, batch_size=args.batch_size,
         model_types=[args.model_type], update_types=[args.update_type],
-        synthetic="nbaiot", synthetic_iid=True, compat=args.compat, backend=args.backend,
+        synthetic=args.data_kind, synthetic_iid=not args.non_iid, compat=args.compat, backend=args.backend,
         global_early_stop=False, save_checkpoints=not args.no_artifacts, output_root=out_root,
         trace_file=args.trace, log_level="WARNING")
     fed = Federation(cfg, args.model_type, args.update_type, run=0, comm=comm,
@@ -139,7 +142,9 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_ROUNDS_PER_SEC, 2),
             "dtype": "fp32",
-            "data": "synthetic (N-BaIoT-shaped, 115 features, IID-10 client sizes); random-init weights",
+            "data": (f"synthetic ({'N-BaIoT' if args.data_kind == 'nbaiot' else 'Kitsune'}-shaped, 115 features, "
+                     f"{'non-IID' if args.non_iid else 'IID'} client mixtures, IID-10 client sizes); "
+                     "random-init weights"),
             "config": {
                 "model": f"SAE 115-27-7-27-115 ({args.model_type}, {args.update_type}), "
                          f"{args.clients_per_gpu} clients/GPU",

@@ -213,3 +213,21 @@ def test_replica_check_passes_and_detects_divergence(tmp_path):
     for t in ts:
         t.join()
     assert len(errs) == 2 and "diverged" in errs[0]
+
+
+REF_CFG = "/root/reference/src/Configuration/scen2-nba-iot-10clients.json"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_CFG), reason="reference data not mounted")
+def test_baseline_config1_reference_csvs_cpu(tmp_path):
+    """BASELINE.json config 1: 2-client SAE FedAvg on CPU from the reference's
+    own scen2 N-BaIoT device list and CSVs (read-only), through main.run_sweep."""
+    import main as driver
+
+    cfg = ExperimentConfig(config_file=REF_CFG, network_size=2, num_rounds=2, epoch=1, batch_size=12,
+                           model_types=["hybrid"], update_types=["avg"], backend="torch", device="cpu",
+                           output_root=str(tmp_path), log_level="WARNING", save_checkpoints=False)
+    best = driver.run_sweep(cfg)
+    assert 0.5 < best["hybrid"]["avg"] <= 1.0
+    summ = json.load(open(os.path.join(cfg.checkpoint_dir, "training_summary.json")))
+    assert summ["best_metrics"]["hybrid"]["avg"] == best["hybrid"]["avg"]
