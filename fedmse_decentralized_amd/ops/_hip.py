@@ -103,7 +103,6 @@ def lib():
                 "fedmx_forward_rows": [vp, i32, vp],
                 "fedmx_weighted_sum": [vp, vp, i32, i32, vp, vp],
                 "fedmx_param_drift": [vp, i32, vp, vp, vp, vp],
-                "fedmx_standardize_ddof1": [vp, i32, i32, vp, vp],
                 "fedmx_standardize_lds": [vp, i32, i32, vp, vp],
                 "fedmx_cen_score": [vp, i32, vp],
                 "fedmx_auc": [vp, i32, vp],

@@ -216,31 +216,6 @@ __global__ __launch_bounds__(1024) void param_drift_kernel(const float* __restri
   }
 }
 
-// ---------------------------------------------------------------------------
-// standardize_ddof1: y = (x - mean) / (std_unbiased + 1e-8) per real column
-// (vote data normalisation, src/Trainer/client_trainer.py:220-223).  One
-// workgroup, one thread per column, float64 accumulation.
-__global__ __launch_bounds__(128) void standardize_kernel(const float* __restrict__ x, int n, int d_in,
-                                                          float* __restrict__ y) {
-  const int col = threadIdx.x;
-  if (col >= DP) return;
-  if (col >= d_in) {
-    for (int r = 0; r < n; ++r) y[(size_t)r * DP + col] = 0.f;
-    return;
-  }
-  double s = 0.0;
-  for (int r = 0; r < n; ++r) s += (double)x[(size_t)r * DP + col];
-  const double mean = s / n;
-  double q = 0.0;
-  for (int r = 0; r < n; ++r) {
-    const double df = (double)x[(size_t)r * DP + col] - mean;
-    q += df * df;
-  }
-  const float stdv = (float)sqrt(q / (n > 1 ? (n - 1) : 1));
-  const float m = (float)mean;
-  const float den = stdv + 1e-8f;
-  for (int r = 0; r < n; ++r) y[(size_t)r * DP + col] = (x[(size_t)r * DP + col] - m) / den;
-}
 
 // Layout probe: D = A*B for A[i][k] = i + 100k, B[k][j] = 1000k + j through
 // the documented lane maps; the host checks D against numpy (asymmetric B
@@ -280,11 +255,6 @@ int fedmx_param_drift(const float* hist, int M, const float* newp, const int* se
                       hipStream_t stream) {
   if (M <= 0) return 0;
   hipLaunchKernelGGL(fedmx::param_drift_kernel, dim3(M), dim3(1024), 0, stream, hist, newp, seg, out);
-  return (int)hipGetLastError();
-}
-
-int fedmx_standardize_ddof1(const float* x, int n, int d_in, float* y, hipStream_t stream) {
-  hipLaunchKernelGGL(fedmx::standardize_kernel, dim3(1), dim3(128), 0, stream, x, n, d_in, y);
   return (int)hipGetLastError();
 }
 
