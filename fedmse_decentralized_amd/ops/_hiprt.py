@@ -119,6 +119,7 @@ class MappedBuffer:
 class _Ring:
     def __init__(self, nbytes: int, stream: int):
         self.buf = MappedBuffer(nbytes)
+        self._retired = []   # replaced buffers stay alive (host views may still point into them)
         self.stream = stream
         self.off = 0
         self.wrap_gen = -1   # generation at which the current pass started
@@ -126,7 +127,13 @@ class _Ring:
     def _alloc(self, nbytes: int) -> int:
         nbytes = (nbytes + 63) & ~63
         if nbytes > self.buf.nbytes:
-            raise ValueError(f"ring request of {nbytes} B exceeds ring size {self.buf.nbytes}")
+            # grow (rare: very large federations): drain every queued user of
+            # the old ring, then replace it with one twice the request
+            device_sync()
+            self._retired.append(self.buf)
+            self.buf = MappedBuffer(2 * nbytes)
+            self.off = 0
+            self.wrap_gen = SyncClock.gen
         if self.off + nbytes > self.buf.nbytes:
             # wrapping: earlier regions may still be read/written by queued kernels
             # unless a stream synchronisation happened since this pass began
