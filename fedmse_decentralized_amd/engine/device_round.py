@@ -9,17 +9,16 @@ can be *enqueued* instead:
 
     train (fused kernel, all local selected clients)
     zero report vectors; standardise vote data; forward + score_reduce -> vec[N,4]
-    [RCCL all-reduce vec]                                 (vote scores, dev MSEs)
+    [pack + ONE RCCL all-gather: the selected models + their vote records]
     elect_kernel            aggregator, cap counts, FedAvg / FedMSE weights
-    [pack + RCCL all-gather of the selected models]
     gather_wsum_kernel      aggregate (bit-identical to the host path)
     forward(agg, every hosted client's verification data) + score_reduce
     param_drift(hist, agg)  per hosted client
     decide_adopt_kernel     ModelVerifier rule + adoption + history update
-    [RCCL all-reduce rejected counts] -> mapped per-round report slot
     snapshot params / best models (one fused device copy)
     side stream: best models -> mapped host snapshot slot, evaluation (fwd + CEN + AUC)
-                 [RCCL all-reduce AUCs] -> report slot; record the round event
+                 [one RCCL all-reduce: AUCs + rejected counts] -> mapped per-round
+                 report slot; record the round event
                  (overlaps the next round's training, which waits only for
                  the snapshot copies)
 
@@ -108,8 +107,9 @@ class DeviceRound:
         self.n_local = len(fed.local)
         self.max_pending = max_pending
         f64, i32, f32 = torch.float64, torch.int32, torch.float32
-        # one buffer for the per-round report vectors: a single fill per round
-        # when ranks sum them (single rank: every entry read is rewritten each round)
+        # vote records [N,4] (every entry the election reads is rewritten each
+        # round) and per-receiver rejected counts (only hosted receivers are
+        # ever written, so other ranks' entries stay zero for the report all-reduce)
         self.red = torch.zeros(5 * N, dtype=f64, device=dev)
         self.vec = self.red[:4 * N].view(N, 4)
         self.rej_vec = self.red[4 * N:5 * N]
@@ -117,7 +117,7 @@ class DeviceRound:
         # training: it reads a snapshot of the parameters taken right after
         # the adoption step, into its own metrics buffer
         self.side = torch.cuda.Stream(device=dev)
-        self.metrics = torch.zeros(N, dtype=f64, device=dev)
+        self.side_rep = torch.zeros(2 * N, dtype=f64, device=dev)   # [AUCs | rejected counts]
         self.eval_params = torch.empty_like(st.params)
         self.best_stage = torch.empty_like(st.best)
         self._ev_side_done = None
@@ -186,8 +186,6 @@ class DeviceRound:
             handle = eng.train_launch(local_rows, fed.hp) if local_sel else None
             rec["handle"] = handle
         with tel.phase("vote"):
-            if comm.world_size > 1:
-                self.red.zero_()
             if local_sel:
                 vs = eng.standardized_vote_data(fed.valid_all[selected[0]])
                 need_dev = self.rule == 1
@@ -201,7 +199,38 @@ class DeviceRound:
                 sse, _ = _hip.forward_rows(st.params, items, fed.dims, True, False)
                 _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs)
         with tel.phase("comm"):
-            comm.all_reduce_inplace(self.vec)
+            if comm.world_size == 1:
+                base = st.params
+                rows = np.asarray([self._loc(c) for c in selected], dtype=np.int64)
+            else:
+                # ONE collective for models and scores: every rank sends its
+                # selected clients' parameter rows plus one extra row carrying
+                # their (vote score, dev MSE) records; the all-gather gives
+                # every rank the whole selection in a world-size independent
+                # order (row strides stay multiples of P for the weighted sum)
+                per_rank: Dict[int, List[int]] = {}
+                for c in selected:
+                    per_rank.setdefault(fed.shard.owner(c), []).append(c)
+                slots = max(len(v) for v in per_rank.values())
+                mine = per_rank.get(comm.rank, [])
+                send = torch.zeros(slots + 1, P_PAD, dtype=torch.float32, device=dev)
+                if mine:
+                    idx = torch.tensor([self._loc(c) for c in mine], dtype=torch.long, device=dev)
+                    send[:len(mine)] = st.params.index_select(0, idx)
+                    cid = torch.tensor(mine, dtype=torch.long, device=dev)
+                    send[slots].view(torch.float64)[:4 * len(mine)].view(-1, 4).copy_(self.vec.index_select(0, cid))
+                allg = comm.all_gather(send).reshape(-1, P_PAD)          # [world * (slots+1), P]
+                tails = allg.view(comm.world_size, slots + 1, P_PAD)[:, slots]
+                recs = tails.contiguous().view(torch.float64)[:, :4 * slots].reshape(comm.world_size * slots, 4)
+                owners = [fed.shard.owner(c) for c in selected]
+                src = torch.tensor([o * slots + per_rank[o].index(c) for o, c in zip(owners, selected)],
+                                   dtype=torch.long, device=dev)
+                dst = torch.tensor(list(selected), dtype=torch.long, device=dev)
+                self.vec.index_copy_(0, dst, recs.index_select(0, src))
+                base = allg
+                rows = np.asarray([o * (slots + 1) + per_rank[o].index(c) for o, c in zip(owners, selected)],
+                                  dtype=np.int64)
+                rec["_keep"] = (allg, send)
         with tel.phase("vote"):
             noise = np.array([fed.noise.rand() for _ in range(k * (k - 1))], dtype=np.float64)
             sel_ptr, noise_ptr = self.rt.desc.put(np.asarray(selected, dtype=np.int32),
@@ -214,24 +243,6 @@ class DeviceRound:
                                rule=self.rule, pad=0)
             _hip.elect(a, dev)
             rec["report"] = rep_view
-        with tel.phase("comm"):
-            if comm.world_size == 1:
-                base = st.params
-                rows = np.asarray([self._loc(c) for c in selected], dtype=np.int64)
-            else:
-                per_rank: Dict[int, List[int]] = {}
-                for c in selected:
-                    per_rank.setdefault(fed.shard.owner(c), []).append(c)
-                slots = max(len(v) for v in per_rank.values())
-                mine = per_rank.get(comm.rank, [])
-                send = torch.zeros(slots, P_PAD, dtype=torch.float32, device=dev)
-                if mine:
-                    idx = torch.tensor([self._loc(c) for c in mine], dtype=torch.long, device=dev)
-                    send[:len(mine)] = st.params.index_select(0, idx)
-                base = comm.all_gather(send).reshape(-1, P_PAD)
-                rows = np.asarray([fed.shard.owner(c) * slots + per_rank[fed.shard.owner(c)].index(c)
-                                   for c in selected], dtype=np.int64)
-                rec["_keep"] = base
         with tel.phase("aggregate"):
             (rows_ptr,) = self.rt.desc.put(rows)
             w = _hip.WsumArgs(base=base.data_ptr(), rows=rows_ptr, weights=self.weights.data_ptr(),
@@ -253,17 +264,17 @@ class DeviceRound:
                                     start=self.start, n_local=self.n_local, P=P_PAD, pad=0)
                 _hip.decide_adopt(d, dev)
         slot_ptr, slot = self.rt.out.take(np.float64, 2 * N)
-        with tel.phase("comm"):
-            comm.all_reduce_inplace(self.rej_vec)
-        _hip.copy_f64(slot_ptr + 8 * N, self.rej_vec.data_ptr(), N, dev)
+        # the previous round's side work has read the snapshot / report buffers
+        if self._ev_side_done is not None:
+            torch.cuda.current_stream(dev).wait_event(self._ev_side_done)
         # snapshot params (for the evaluation) and the best models (for the
         # artefacts) on the main stream: one fused device copy, so the next
-        # round's training can start right away
-        if self._ev_side_done is not None:   # the previous round's side work has read the snapshots
-            torch.cuda.current_stream(dev).wait_event(self._ev_side_done)
+        # round's training can start right away; the rejected counts go to the
+        # side stream's report buffer ([metrics | rejected])
         nd = st.params.numel() // 2
         _hip.copy2_f64(self.eval_params.data_ptr(), st.params.data_ptr(), nd,
                        self.best_stage.data_ptr(), st.best.data_ptr(), nd, dev)
+        _hip.copy_f64(self.side_rep.data_ptr() + 8 * N, self.rej_vec.data_ptr(), N, dev)
         ev_dec = torch.cuda.Event()
         ev_dec.record()
         with tel.phase("eval"), _hip.on_stream(self.side):
@@ -280,13 +291,14 @@ class DeviceRound:
             eng.evaluate_launch(fed.model_type, params=self.eval_params)
             aucs_ptr = eng._plan(fed.model_type, self.eval_params)["aucs_buf"].dev_ptr
             if comm.world_size == 1:
-                _hip.copy_f64(slot_ptr, aucs_ptr, N, dev)
+                _hip.copy2_f64(slot_ptr, aucs_ptr, N, slot_ptr + 8 * N, self.side_rep.data_ptr() + 8 * N, N, dev)
             else:
-                self.metrics.zero_()
+                # [AUCs | rejected counts]: one RCCL all-reduce, off the main stream
+                self.side_rep[:N].zero_()
                 if self.n_local:
-                    _hip.copy_f64(self.metrics.data_ptr() + 8 * self.start, aucs_ptr, self.n_local, dev)
-                comm.all_reduce_inplace(self.metrics)
-                _hip.copy_f64(slot_ptr, self.metrics.data_ptr(), N, dev)
+                    _hip.copy_f64(self.side_rep.data_ptr() + 8 * self.start, aucs_ptr, self.n_local, dev)
+                comm.all_reduce_inplace(self.side_rep)
+                _hip.copy_f64(slot_ptr, self.side_rep.data_ptr(), 2 * N, dev)
             ev = torch.cuda.Event()
             ev.record(self.side)
             self._ev_side_done = ev
