@@ -92,6 +92,7 @@ class ExperimentConfig:
     thesis_loss_ratio: float = 0.1
     thesis_vote_mse_cap: float = 3.0
     fusion_max_rows: int = 1024          # dev rows used by the fusion_avg KDE similarity
+    fedavg_sample_weighted: bool = False  # FedAvg weights ∝ training-set size (reference: plain mean, Q13)
     # experiment-level parallelism: with N ranks, combination
     # i of the model_type x update_type x run sweep runs on rank i % N (each
     # as a single-rank federation on that rank's GPU) instead of every

@@ -64,6 +64,7 @@ def fast_path_supported(fed) -> Optional[str]:
         (not cfg.malicious_clients and not cfg.dropped_clients, "fault injection is enabled"),
         (not cfg.save_latents, "latent logging is enabled"),
         (not cfg.resume and not cfg.snapshot_every, "resume snapshots are enabled"),
+        (not cfg.fedavg_sample_weighted, "sample-weighted FedAvg"),
         (cfg.device_protocol, "device protocol disabled"),
     ]
     for ok, why in checks:

@@ -388,7 +388,9 @@ class Federation:
                 sim = None
                 if self.update_type == "fusion_avg":
                     sim = self._fusion_similarity(selected)
-                plan = make_plan(self.update_type, selected, aggregator, dev_mse, cfg.compat, sim=sim)
+                ns = {c: self.clients[c].train.shape[0] for c in selected} if cfg.fedavg_sample_weighted else None
+                plan = make_plan(self.update_type, selected, aggregator, dev_mse, cfg.compat, sim=sim,
+                                 num_samples=ns)
             with self.tel.phase("comm"):
                 stack = self._gather_params([c for c, _ in plan], selected)
             with self.tel.phase("aggregate"):

@@ -30,9 +30,15 @@ from typing import Dict, List, Sequence, Tuple
 Plan = List[Tuple[int, float]]
 
 
-def plan_mean(selected: Sequence[int]) -> Plan:
-    k = len(selected)
-    return [(cid, 1.0 / k) for cid in selected]
+def plan_mean(selected: Sequence[int], num_samples: Dict[int, float] = None) -> Plan:
+    """FedAvg / FedProx.  The reference passes ``num_samples = 1.0`` for every
+    model (Q13), i.e. a plain mean; ``num_samples`` (client -> training-set
+    size) gives the textbook sample-weighted FedAvg instead."""
+    if num_samples is None:
+        k = len(selected)
+        return [(cid, 1.0 / k) for cid in selected]
+    tot = sum(float(num_samples[c]) for c in selected)
+    return [(cid, float(num_samples[cid]) / tot) for cid in selected]
 
 
 def plan_mse_avg(selected: Sequence[int], aggregator: int, dev_mse: Dict[int, float], compat: str = "reference") -> Plan:
@@ -68,9 +74,9 @@ UPDATE_TYPES = ("avg", "fedprox", "mse_avg", "fusion_avg")
 
 
 def make_plan(update_type: str, selected: Sequence[int], aggregator: int, dev_mse: Dict[int, float] = None,
-              compat: str = "reference", sim: Dict[int, float] = None) -> Plan:
+              compat: str = "reference", sim: Dict[int, float] = None, num_samples: Dict[int, float] = None) -> Plan:
     if update_type in ("avg", "fedprox"):
-        return plan_mean(selected)
+        return plan_mean(selected, num_samples)
     if update_type == "mse_avg":
         return plan_mse_avg(selected, aggregator, dev_mse, compat)
     if update_type == "fusion_avg":

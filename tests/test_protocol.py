@@ -136,3 +136,11 @@ def test_early_stop_compat_vs_fixed():
     assert fx.update(0.94)
     fx.start_combination()
     assert not fx.update(0.5)
+
+
+def test_sample_weighted_fedavg_plan():
+    from fedmse_decentralized_amd.protocol.aggregation import make_plan
+
+    plan = make_plan("avg", [2, 0, 1], 0, num_samples={0: 100, 1: 300, 2: 600})
+    assert plan == [(2, 0.6), (0, 0.1), (1, 0.3)]
+    assert make_plan("fedprox", [2, 0], 0) == [(2, 0.5), (0, 0.5)]
