@@ -8,19 +8,18 @@ a host RNG whose consumption does not depend on results, so the whole round
 can be *enqueued* instead:
 
     train (fused kernel, all local selected clients)
-    zero report vectors; standardise vote data; forward + score_reduce -> vec[N,4]
+    standardise vote data; forward + score_reduce -> vec[N,4] (vote score, dev MSE)
     [pack + ONE RCCL all-gather: the selected models + their vote records]
-    elect_kernel            aggregator, cap counts, FedAvg / FedMSE weights
-    gather_wsum_kernel      aggregate (bit-identical to the host path)
-    forward(agg, every hosted client's verification data) + score_reduce
-    param_drift(hist, agg)  per hosted client
-    decide_adopt_kernel     ModelVerifier rule + adoption + history update
+    elect_wsum_kernel       aggregator, FedAvg / FedMSE weights, aggregate
+    forward(agg, every hosted client's verification data)
+    decide_adopt_kernel     MSE + drift reductions, ModelVerifier rule, adoption,
+                            history update, aggregation-cap count
     snapshot params / best models (one fused device copy)
     side stream: best models -> mapped host snapshot slot, evaluation (fwd + CEN + AUC)
                  [one RCCL all-reduce: AUCs + rejected counts] -> mapped per-round
                  report slot; record the round event
-                 (overlaps the next round's training, which waits only for
-                 the snapshot copies)
+                 (overlaps the next round's training; the next round's
+                 verification waits for it before reusing the buffers)
 
 and the host moves on to the next round.  Results are *collected* later
 (at most ``max_pending`` rounds behind, or when a caller reads a round's
@@ -108,17 +107,15 @@ class DeviceRound:
         self.n_local = len(fed.local)
         self.max_pending = max_pending
         f64, i32, f32 = torch.float64, torch.int32, torch.float32
-        # vote records [N,4] (every entry the election reads is rewritten each
-        # round) and per-receiver rejected counts (only hosted receivers are
-        # ever written, so other ranks' entries stay zero for the report all-reduce)
-        self.red = torch.zeros(5 * N, dtype=f64, device=dev)
-        self.vec = self.red[:4 * N].view(N, 4)
-        self.rej_vec = self.red[4 * N:5 * N]
+        # vote records [N,4]: every entry the election reads is rewritten each round
+        self.vec = torch.zeros(N, 4, dtype=f64, device=dev)
         # evaluation runs on a side stream and overlaps the next round's
         # training: it reads a snapshot of the parameters taken right after
         # the adoption step, into its own metrics buffer
         self.side = torch.cuda.Stream(device=dev)
-        self.side_rep = torch.zeros(2 * N, dtype=f64, device=dev)   # [AUCs | rejected counts]
+        # [AUCs | rejected counts]; only hosted receivers' counts are ever
+        # written, so other ranks' entries stay zero for the report all-reduce
+        self.side_rep = torch.zeros(2 * N, dtype=f64, device=dev)
         self.eval_params = torch.empty_like(st.params)
         self.best_stage = torch.empty_like(st.best)
         self._ev_side_done = None
@@ -145,8 +142,6 @@ class DeviceRound:
         self.has_hist = torch.zeros(n, dtype=i32, device=dev)
         self.hist_perf = torch.zeros(n, dtype=f64, device=dev)
         self.rejected = torch.zeros(n, dtype=i32, device=dev)
-        self.mse = torch.zeros(n, 2, dtype=f64, device=dev)
-        self.drift = torch.zeros(n, dtype=f32, device=dev)
         self.rt = _hip.runtime(dev)
         cfg = fed.cfg
         # verification: the aggregate on every hosted client's verification data (fixed mode: own V)
@@ -157,8 +152,8 @@ class DeviceRound:
         self.vplan = _hip.FwdPlan(self.agg.unsqueeze(0), [(0, d) for d in vdata], fed.dims,
                                   want_sse=True, want_latent=False) if fed.local else None
         if fed.local:
-            self.vseg = _hip.seg_desc_device(self.vplan.sse_views(), [0] * self.n_local,
-                                             self.mse.data_ptr() + 16 * np.arange(self.n_local), dev)
+            self.vsse_off = torch.from_numpy(self.vplan.offs.astype(np.int32)).to(dev)
+            self.vsse_n = torch.from_numpy(self.vplan.sizes.astype(np.int32)).to(dev)
         self.rule = 1 if fed.update_type == "mse_avg" else 0
         self.pending: deque = deque()
         self.all_rounds: Dict[int, dict] = {}
@@ -232,50 +227,48 @@ class DeviceRound:
                 rows = np.asarray([o * (slots + 1) + per_rank[o].index(c) for o, c in zip(owners, selected)],
                                   dtype=np.int64)
                 rec["_keep"] = (allg, send)
-        with tel.phase("vote"):
+        with tel.phase("aggregate"):
             noise = np.array([fed.noise.rand() for _ in range(k * (k - 1))], dtype=np.float64)
-            sel_ptr, noise_ptr = self.rt.desc.put(np.asarray(selected, dtype=np.int32),
-                                                  noise if noise.size else np.zeros(1))
+            sel_ptr, noise_ptr, rows_ptr = self.rt.desc.put(np.asarray(selected, dtype=np.int32),
+                                                            noise if noise.size else np.zeros(1), rows)
             rep_ptr, rep_view = self.rt.out.take(np.int32, 2)
             rep_view[:] = -2
             a = _hip.ElectArgs(sel=sel_ptr, vec=self.vec.data_ptr(), noise=noise_ptr,
                                agg_counts=self.agg_counts.data_ptr(), weights=self.weights.data_ptr(),
                                state=self.state.data_ptr(), report=rep_ptr, k=k, cap=cfg.max_aggregation,
                                rule=self.rule, pad=0)
-            _hip.elect(a, dev)
-            rec["report"] = rep_view
-        with tel.phase("aggregate"):
-            (rows_ptr,) = self.rt.desc.put(rows)
             w = _hip.WsumArgs(base=base.data_ptr(), rows=rows_ptr, weights=self.weights.data_ptr(),
                               state=self.state.data_ptr(), out=self.agg.data_ptr(), k=k, P=P_PAD)
-            _hip.gather_wsum(w, dev)
-        with tel.phase("verify"):
-            if self.n_local:
-                self.vplan.run()
-                _hip.launch_score_reduce(self.vseg, self.n_local, fed.dims.d_in, dev)
-                _hip._check(_hip.lib().fedmx_param_drift(self.hist.data_ptr(), self.n_local, self.agg.data_ptr(),
-                                                         eng._seg.data_ptr(), self.drift.data_ptr(), self.rt.stream),
-                            "fedmx_param_drift")
-                d = _hip.DecideArgs(params=st.params.data_ptr(), anchor=st.anchor.data_ptr(),
-                                    hist=self.hist.data_ptr(), agg=self.agg.data_ptr(), state=self.state.data_ptr(),
-                                    mse=self.mse.data_ptr(), drift=self.drift.data_ptr(),
-                                    has_hist=self.has_hist.data_ptr(), hist_perf=self.hist_perf.data_ptr(),
-                                    rejected=self.rejected.data_ptr(), rej_vec=self.rej_vec.data_ptr(),
-                                    thr=float(cfg.verification_threshold), pthr=float(cfg.performance_threshold),
-                                    start=self.start, n_local=self.n_local, P=P_PAD, pad=0)
-                _hip.decide_adopt(d, dev)
-        slot_ptr, slot = self.rt.out.take(np.float64, 2 * N)
+            _hip.elect_wsum(a, w, dev)
+            rec["report"] = rep_view
         # the previous round's side work has read the snapshot / report buffers
         if self._ev_side_done is not None:
             torch.cuda.current_stream(dev).wait_event(self._ev_side_done)
+        with tel.phase("verify"):
+            # every hosted receiver: the aggregate's SSE rows on its data, then
+            # one kernel reduces MSE + drift, decides, adopts and bumps the cap
+            # count; rejected counts go straight into the side stream's report
+            # buffer ([AUCs | rejected])
+            if self.n_local:
+                self.vplan.run()
+            d = _hip.DecideArgs(params=st.params.data_ptr(), anchor=st.anchor.data_ptr(),
+                                hist=self.hist.data_ptr(), agg=self.agg.data_ptr(), state=self.state.data_ptr(),
+                                sse=self.vplan.sse.data_ptr() if self.n_local else 0,
+                                sse_off=self.vsse_off.data_ptr() if self.n_local else 0,
+                                sse_n=self.vsse_n.data_ptr() if self.n_local else 0,
+                                seg=eng._seg.data_ptr(), agg_counts=self.agg_counts.data_ptr(),
+                                has_hist=self.has_hist.data_ptr(), hist_perf=self.hist_perf.data_ptr(),
+                                rejected=self.rejected.data_ptr(), rej_out=self.side_rep.data_ptr() + 8 * N,
+                                thr=float(cfg.verification_threshold), pthr=float(cfg.performance_threshold),
+                                start=self.start, n_local=self.n_local, P=P_PAD, d_in=fed.dims.d_in)
+            _hip.decide_adopt(d, dev)
+        slot_ptr, slot = self.rt.out.take(np.float64, 2 * N)
         # snapshot params (for the evaluation) and the best models (for the
         # artefacts) on the main stream: one fused device copy, so the next
-        # round's training can start right away; the rejected counts go to the
-        # side stream's report buffer ([metrics | rejected])
+        # round's training can start right away
         nd = st.params.numel() // 2
         _hip.copy2_f64(self.eval_params.data_ptr(), st.params.data_ptr(), nd,
                        self.best_stage.data_ptr(), st.best.data_ptr(), nd, dev)
-        _hip.copy_f64(self.side_rep.data_ptr() + 8 * N, self.rej_vec.data_ptr(), N, dev)
         ev_dec = torch.cuda.Event()
         ev_dec.record()
         with tel.phase("eval"), _hip.on_stream(self.side):

@@ -81,10 +81,11 @@ class WsumArgs(ctypes.Structure):
 
 
 class DecideArgs(ctypes.Structure):
-    _fields_ = [("params", _vp), ("anchor", _vp), ("hist", _vp), ("agg", _vp), ("state", _vp), ("mse", _vp),
-                ("drift", _vp), ("has_hist", _vp), ("hist_perf", _vp), ("rejected", _vp), ("rej_vec", _vp),
+    _fields_ = [("params", _vp), ("anchor", _vp), ("hist", _vp), ("agg", _vp), ("state", _vp), ("sse", _vp),
+                ("sse_off", _vp), ("sse_n", _vp), ("seg", _vp), ("agg_counts", _vp), ("has_hist", _vp),
+                ("hist_perf", _vp), ("rejected", _vp), ("rej_out", _vp),
                 ("thr", ctypes.c_double), ("pthr", ctypes.c_double), ("start", _i32), ("n_local", _i32),
-                ("P", _i32), ("pad", _i32)]
+                ("P", _i32), ("d_in", _i32)]
 
 
 def lib():
@@ -111,8 +112,7 @@ def lib():
                 "fedmx_train": [ctypes.POINTER(TrainArgs), i32, vp],
                 "fedmx_train8": [ctypes.POINTER(TrainArgs), i32, vp],
                 "fedmx_probe_mfma": [vp, vp],
-                "fedmx_elect": [ctypes.POINTER(ElectArgs), vp],
-                "fedmx_gather_wsum": [ctypes.POINTER(WsumArgs), vp],
+                "fedmx_elect_wsum": [ctypes.POINTER(ElectArgs), ctypes.POINTER(WsumArgs), vp],
                 "fedmx_decide_adopt": [ctypes.POINTER(DecideArgs), vp],
                 "fedmx_copy_f64": [vp, vp, i32, vp],
                 "fedmx_copy2_f64": [vp, vp, i32, vp, vp, i32, vp],
@@ -387,12 +387,8 @@ def launch_score_reduce(desc_dev: torch.Tensor, n: int, d_in: int, device):
     _check(lib().fedmx_score_reduce(desc_dev.data_ptr(), n, d_in, _stream(device)), "fedmx_score_reduce")
 
 
-def elect(args: ElectArgs, device):
-    _check(lib().fedmx_elect(ctypes.byref(args), _stream(device)), "fedmx_elect")
-
-
-def gather_wsum(args: WsumArgs, device):
-    _check(lib().fedmx_gather_wsum(ctypes.byref(args), _stream(device)), "fedmx_gather_wsum")
+def elect_wsum(eargs: ElectArgs, wargs: WsumArgs, device):
+    _check(lib().fedmx_elect_wsum(ctypes.byref(eargs), ctypes.byref(wargs), _stream(device)), "fedmx_elect_wsum")
 
 
 def decide_adopt(args: DecideArgs, device):

@@ -3,15 +3,16 @@
 // read their inputs from device memory, so a whole federated round is one
 // stream of launches with no host round trip.
 //
-//  * elect_kernel        : aggregator election (src/Trainer/client_trainer.py:249-285,
-//                          driver src/main.py:281-288) over the all-reduced
-//                          vote scores and a host-drawn noise table, the
-//                          aggregation-cap bookkeeping (:78, :279, :300-303)
-//                          and the FedAvg / FedMSE weights (:107-130)
-//  * gather_wsum_kernel  : sum_j w_j * theta_{row_j} in selection order, the
-//                          same separately-rounded fp32 order as
-//                          weighted_sum_kernel (bit-identical aggregate)
-//  * decide_adopt_kernel : ModelVerifier rule (src/Trainer/model_verifier.py:72-99)
+//  * elect_wsum_kernel   : aggregator election (src/Trainer/client_trainer.py:249-285,
+//                          driver src/main.py:281-288) over the gathered vote
+//                          scores and a host-drawn noise table, the FedAvg /
+//                          FedMSE weights (:107-130), and the aggregate
+//                          sum_j w_j * theta_{row_j} in selection order with the
+//                          separately-rounded fp32 order of weighted_sum_kernel
+//                          (bit-identical aggregate)
+//  * decide_adopt_kernel : aggregation-cap bookkeeping (:78, :279, :300-303),
+//                          verification MSE + parameter drift reductions and
+//                          the ModelVerifier rule (src/Trainer/model_verifier.py:72-99)
 //                          per hosted receiver + update_from_peers adoption
 //                          (client_trainer.py:174-206): accepted receivers load
 //                          the aggregate and re-anchor FedProx, the history is
@@ -36,46 +37,6 @@ struct ElectArgs {
 };
 static_assert(sizeof(ElectArgs) == 72, "ElectArgs layout is shared with Python");
 
-__global__ void elect_kernel(const ElectArgs A) {
-  if (threadIdx.x != 0) return;
-  int agg = -1, voter = -1;
-  for (int vi = 0; vi < A.k && agg < 0; ++vi) {
-    const int v = A.sel[vi];
-    const double* u = A.noise + (size_t)vi * (A.k - 1);
-    int best = -1, j = 0;
-    double best_s = 0.0;
-    for (int ci = 0; ci < A.k; ++ci) {
-      const int c = A.sel[ci];
-      if (c == v) continue;
-      const double f = 1.0 + (u[j++] - 0.5) * 0.0002;
-      const double s = A.vec[(size_t)c * 4] * f;
-      // ascending stable sort, first candidate below the cap
-      if (A.agg_counts[c] < A.cap && (best < 0 || s < best_s)) {
-        best = c;
-        best_s = s;
-      }
-    }
-    if (best >= 0) {
-      agg = best;
-      voter = v;
-    }
-  }
-  A.state[0] = agg;
-  A.state[1] = voter;
-  A.report[0] = agg;
-  A.report[1] = voter;
-  if (agg < 0) return;
-  A.agg_counts[agg] += 1;
-  if (A.rule == 1) {
-    double tot = 0.0;
-    for (int j = 0; j < A.k; ++j) tot += 1.0 / A.vec[(size_t)A.sel[j] * 4 + 3];
-    for (int j = 0; j < A.k; ++j) A.weights[j] = (float)((1.0 / A.vec[(size_t)A.sel[j] * 4 + 3]) / tot);
-  } else {
-    const float w = (float)(1.0 / (double)A.k);
-    for (int j = 0; j < A.k; ++j) A.weights[j] = w;
-  }
-}
-
 struct WsumArgs {
   const float* base;       // row-major [*, P]
   const int64_t* rows;     // [k] source rows (selection order)
@@ -86,18 +47,69 @@ struct WsumArgs {
 };
 static_assert(sizeof(WsumArgs) == 48, "WsumArgs layout is shared with Python");
 
-__global__ __launch_bounds__(256) void gather_wsum_kernel(const WsumArgs A) {
-  if (A.state[0] < 0) return;
+// Election and aggregation in one launch: every workgroup replays the
+// (tiny, k <= a few hundred) election from the same inputs — identical
+// results, no inter-block communication — then reduces its slice of the
+// aggregate.  Workgroup 0 publishes the aggregator / voter / weights; the
+// aggregation-cap count is bumped later by decide_adopt (a single writer,
+// after every workgroup here has read the counts).
+__global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, const WsumArgs W) {
+  __shared__ float s_w[1024];
+  __shared__ int s_agg;
+  if (threadIdx.x == 0) {
+    int agg = -1, voter = -1;
+    for (int vi = 0; vi < E.k && agg < 0; ++vi) {
+      const int v = E.sel[vi];
+      const double* u = E.noise + (size_t)vi * (E.k - 1);
+      int best = -1, j = 0;
+      double best_s = 0.0;
+      for (int ci = 0; ci < E.k; ++ci) {
+        const int c = E.sel[ci];
+        if (c == v) continue;
+        const double f = 1.0 + (u[j++] - 0.5) * 0.0002;
+        const double sc = E.vec[(size_t)c * 4] * f;
+        if (E.agg_counts[c] < E.cap && (best < 0 || sc < best_s)) {
+          best = c;
+          best_s = sc;
+        }
+      }
+      if (best >= 0) {
+        agg = best;
+        voter = v;
+      }
+    }
+    s_agg = agg;
+    if (agg >= 0) {
+      if (E.rule == 1) {
+        double tot = 0.0;
+        for (int j = 0; j < E.k; ++j) tot += 1.0 / E.vec[(size_t)E.sel[j] * 4 + 3];
+        for (int j = 0; j < E.k; ++j) s_w[j] = (float)((1.0 / E.vec[(size_t)E.sel[j] * 4 + 3]) / tot);
+      } else {
+        const float w = (float)(1.0 / (double)E.k);
+        for (int j = 0; j < E.k; ++j) s_w[j] = w;
+      }
+    }
+    if (blockIdx.x == 0) {
+      E.state[0] = agg;
+      E.state[1] = voter;
+      E.report[0] = agg;
+      E.report[1] = voter;
+      if (agg >= 0)
+        for (int j = 0; j < E.k; ++j) E.weights[j] = s_w[j];
+    }
+  }
+  __syncthreads();
+  if (s_agg < 0) return;
   const int i = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i >= A.P) return;
+  if (i >= W.P) return;
   f32x4 acc = zero4();
-  for (int k = 0; k < A.k; ++k) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(A.base + (size_t)A.rows[k] * A.P + i);
-    const float wk = A.weights[k];
+  for (int k = 0; k < W.k; ++k) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(W.base + (size_t)W.rows[k] * W.P + i);
+    const float wk = s_w[k];
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[r] = (k == 0) ? __fmul_rn(v[r], wk) : __fadd_rn(acc[r], __fmul_rn(v[r], wk));
   }
-  *reinterpret_cast<f32x4*>(A.out + i) = acc;
+  *reinterpret_cast<f32x4*>(W.out + i) = acc;
 }
 
 struct DecideArgs {
@@ -106,23 +118,35 @@ struct DecideArgs {
   float* hist;             // [n_local, P] last received aggregate
   const float* agg;        // [P]
   const int32_t* state;    // aggregator
-  const double* mse;       // [n_local][2] score_reduce output; [.][1] = MSE of agg on the receiver's data
-  const float* drift;      // [n_local] drift of hist vs agg
+  const float* sse;        // verification forward: per-row SSE of agg on each receiver's data
+  const int32_t* sse_off;  // [n_local] row offset of receiver cl's segment in sse
+  const int32_t* sse_n;    // [n_local] rows of that segment
+  const int32_t* seg;      // [P] state-dict tensor id of each padded slot (-1 = padding)
+  int32_t* agg_counts;     // [N] aggregation-cap counts (bumped here, workgroup 0)
   int32_t* has_hist;       // [n_local]
   double* hist_perf;       // [n_local]
   int32_t* rejected;       // [n_local]
-  double* rej_vec;         // [N] out: rejected count per receiver (global id)
+  double* rej_out;         // [N] rejected count per receiver (global id)
   double thr, pthr;
-  int32_t start, n_local, P, pad;
+  int32_t start, n_local, P, d_in;
 };
-static_assert(sizeof(DecideArgs) == 120, "DecideArgs layout is shared with Python");
+static_assert(sizeof(DecideArgs) == 144, "DecideArgs layout is shared with Python");
 
-__global__ __launch_bounds__(256) void decide_adopt_kernel(const DecideArgs A) {
+// One 1024-thread workgroup per hosted client.  The verification MSE and the
+// parameter drift are reduced here with exactly the arithmetic of
+// score_reduce_kernel (threads 0..255) and param_drift_kernel (all 1024
+// threads), so decisions are bit-identical to the host-decision path.
+__global__ __launch_bounds__(1024) void decide_adopt_kernel(const DecideArgs A) {
   const int a = A.state[0];
   if (a < 0) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.agg_counts[a] += 1;
   const int cl = blockIdx.x;
+  if (cl >= A.n_local) return;
   const int c = A.start + cl;
+  const int had_hist = A.has_hist[cl];  // read by every thread before thread 0 updates it
   __shared__ int s_ok;
+  __shared__ double s_d[4];
+  __shared__ float part[8][16];
   const size_t off = (size_t)cl * A.P;
   const f32x4* src = reinterpret_cast<const f32x4*>(A.agg);
   const int n4 = A.P / 4;
@@ -130,25 +154,71 @@ __global__ __launch_bounds__(256) void decide_adopt_kernel(const DecideArgs A) {
     for (int i = threadIdx.x; i < n4; i += blockDim.x) reinterpret_cast<f32x4*>(A.params + off)[i] = src[i];
     return;
   }
-  if (threadIdx.x == 0) {
-    const double perf = 1.0 / (1.0 + A.mse[(size_t)cl * 2 + 1]);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  // ---- MSE of the aggregate on this receiver's data (score_reduce, one batch)
+  double mse = 0.0;
+  {
+    const float* sp = A.sse + A.sse_off[cl];
+    const int n = A.sse_n[cl];
+    double sv = 0.0;
+    if (tid < 256)
+      for (int r = tid; r < n; r += 256) sv += (double)sp[r];
+    for (int o = 32; o >= 1; o >>= 1) sv += __shfl_xor(sv, o, 64);
+    if (lane == 0 && wv < 4) s_d[wv] = sv;
+    __syncthreads();
+    const double tot = s_d[0] + s_d[1] + s_d[2] + s_d[3];
+    mse = n > 0 ? tot / ((double)n * A.d_in) : __builtin_nan("");
+  }
+  // ---- drift of the receiver's history vs the aggregate (param_drift)
+  float drift = 0.f;
+  if (had_hist) {
+    const float* h = A.hist + off;
+    float acc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = 0.f;
+    for (int p = tid; p < A.P; p += blockDim.x) {
+      const int sg = A.seg[p];
+      const float df = h[p] - A.agg[p];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] += (sg == t) ? df * df : 0.0f;
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float v = wave_sum(acc[t]);
+      if (lane == 0) part[t][wv] = v;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const int nw = blockDim.x >> 6;
+      float tot = 0.f;
+      for (int t = 0; t < 8; ++t) {
+        float s2 = 0.f;
+        for (int w = 0; w < nw; ++w) s2 += part[t][w];
+        tot += sqrtf(s2);
+      }
+      drift = tot;
+    }
+  }
+  if (tid == 0) {
+    const double perf = 1.0 / (1.0 + mse);
     int ok;
-    if (!A.has_hist[cl]) {
+    if (!had_hist) {
       ok = 1;  // the first received model is accepted unconditionally
       A.has_hist[cl] = 1;
     } else {
       const double change = perf - A.hist_perf[cl];
-      ok = ((double)A.drift[cl] <= A.thr) && (change >= -A.pthr);
+      ok = ((double)drift <= A.thr) && (change >= -A.pthr);
     }
     A.hist_perf[cl] = perf;
     const int rj = ok ? 0 : A.rejected[cl] + 1;
     A.rejected[cl] = rj;
-    A.rej_vec[c] = (double)rj;
+    A.rej_out[c] = (double)rj;
     s_ok = ok;
   }
   __syncthreads();
   const bool ok = s_ok != 0;
-  for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+  for (int i = tid; i < n4; i += blockDim.x) {
     const f32x4 v = src[i];
     reinterpret_cast<f32x4*>(A.hist + off)[i] = v;
     if (ok) {
@@ -187,24 +257,20 @@ int fedmx_copy2_f64(double* d0, const double* s0, int n0, double* d1, const doub
   return (int)hipGetLastError();
 }
 
-int fedmx_elect(const void* args, hipStream_t stream) {
-  hipLaunchKernelGGL(fedmx::elect_kernel, dim3(1), dim3(64), 0, stream, *reinterpret_cast<const fedmx::ElectArgs*>(args));
-  return (int)hipGetLastError();
-}
-
-int fedmx_gather_wsum(const void* args, hipStream_t stream) {
-  const fedmx::WsumArgs& A = *reinterpret_cast<const fedmx::WsumArgs*>(args);
-  if (A.P % 4 != 0 || A.k < 1) return -1;
-  const int n4 = A.P / 4;
-  hipLaunchKernelGGL(fedmx::gather_wsum_kernel, dim3((n4 + 255) / 256), dim3(256), 0, stream, A);
-  return (int)hipGetLastError();
-}
-
 int fedmx_decide_adopt(const void* args, hipStream_t stream) {
   const fedmx::DecideArgs& A = *reinterpret_cast<const fedmx::DecideArgs*>(args);
-  if (A.n_local <= 0) return 0;
-  if (A.P % 4 != 0) return -1;
-  hipLaunchKernelGGL(fedmx::decide_adopt_kernel, dim3(A.n_local), dim3(256), 0, stream, A);
+  if (A.P % 4 != 0 || A.P != fedmx::P_PAD) return -1;
+  // at least one workgroup: it bumps the replicated aggregation-cap count
+  hipLaunchKernelGGL(fedmx::decide_adopt_kernel, dim3(A.n_local > 0 ? A.n_local : 1), dim3(1024), 0, stream, A);
+  return (int)hipGetLastError();
+}
+
+int fedmx_elect_wsum(const void* eargs, const void* wargs, hipStream_t stream) {
+  const fedmx::ElectArgs& E = *reinterpret_cast<const fedmx::ElectArgs*>(eargs);
+  const fedmx::WsumArgs& W = *reinterpret_cast<const fedmx::WsumArgs*>(wargs);
+  if (W.P % 4 != 0 || W.k < 1 || E.k > 1024) return -1;
+  const int n4 = W.P / 4;
+  hipLaunchKernelGGL(fedmx::elect_wsum_kernel, dim3((n4 + 255) / 256), dim3(256), 0, stream, E, W);
   return (int)hipGetLastError();
 }
 
