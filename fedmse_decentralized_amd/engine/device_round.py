@@ -8,7 +8,8 @@ a host RNG whose consumption does not depend on results, so the whole round
 can be *enqueued* instead:
 
     train (fused kernel, all local selected clients)
-    standardise vote data; forward + score_reduce -> vec[N,4] (vote score, dev MSE)
+    (side stream, overlapping training: standardise the vote data)
+    forward + score_reduce -> vec[N,4] (vote score, dev MSE)
     [pack + ONE RCCL all-gather: the selected models + their vote records]
     elect_wsum_kernel       aggregator, FedAvg / FedMSE weights, aggregate
     forward(agg, every hosted client's verification data)
@@ -119,6 +120,8 @@ class DeviceRound:
         self.eval_params = torch.empty_like(st.params)
         self.best_stage = torch.empty_like(st.best)
         self._ev_side_done = None
+        self.vs_bufs = [None, None]       # standardised vote data, by round parity
+        self._ev_vote = [None, None]
         # best-model snapshots for the artefact writer: a ring of mapped host
         # slots filled by a device copy kernel (no torch pinned allocation or
         # blocking copy on the enqueue path); a slot is reused once the writer
@@ -178,12 +181,28 @@ class DeviceRound:
         local_rows = [self._loc(c) for c in local_sel]
         rec = dict(round=rnd, selected=list(selected), local_sel=local_sel, done=False)
 
+        ev_std = None
+        if local_sel:
+            # the vote data does not depend on training: standardise it on the
+            # side stream (double-buffered by round parity) while training runs
+            vdata = fed.valid_all[selected[0]]
+            pb = rnd & 1
+            if self.vs_bufs[pb] is None or self.vs_bufs[pb].shape[0] < vdata.shape[0]:
+                self.vs_bufs[pb] = torch.empty(max(vdata.shape[0], 256), vdata.shape[1], dtype=torch.float32,
+                                               device=dev)
+            vs = self.vs_bufs[pb][:vdata.shape[0]]
+            with _hip.on_stream(self.side):
+                if self._ev_vote[pb] is not None:   # round r-2's vote forward has read this buffer
+                    self.side.wait_event(self._ev_vote[pb])
+                _hip.standardize_ddof1(vdata.contiguous(), fed.dims.d_in, out=vs)
+                ev_std = torch.cuda.Event()
+                ev_std.record(self.side)
         with tel.phase("train"):
             handle = eng.train_launch(local_rows, fed.hp) if local_sel else None
             rec["handle"] = handle
         with tel.phase("vote"):
             if local_sel:
-                vs = eng.standardized_vote_data(fed.valid_all[selected[0]])
+                torch.cuda.current_stream(dev).wait_event(ev_std)
                 need_dev = self.rule == 1
                 items = [(r, vs) for r in local_rows]
                 outs = [self.vec[c].data_ptr() for c in local_sel]
@@ -193,6 +212,8 @@ class DeviceRound:
                     outs += [self.vec[c].data_ptr() + 16 for c in local_sel]
                     batch += [0] * len(local_rows)
                 sse, _ = _hip.forward_rows(st.params, items, fed.dims, True, False)
+                self._ev_vote[pb] = torch.cuda.Event()
+                self._ev_vote[pb].record()
                 _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs)
         with tel.phase("comm"):
             if comm.world_size == 1:

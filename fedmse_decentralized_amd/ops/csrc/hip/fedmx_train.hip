@@ -296,7 +296,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   // Rest of the forward of one chunk: layer-1 K reduction through LDS
   // (barrier #1), layers 2-3 (redundant per wave), layer 4 on own rows.  Adds
   // this lane's loss share (MSE of its own 32 features; shrink term on wave 0 /
-  // lane group 0), normalised by the whole batch's row count bt.
+  // lane group 0), normalised by the whole batch's row count bt.  Validation
+  // keeps one tile per batch (no packing across batch boundaries): the loss
+  // sums then follow the reference's per-batch order closely enough that the
+  // patience decisions match it (a packed variant flipped a near-tie).
   auto forward_rest = [&](const f32x4& acc0, const f32x4& acc1, const XChunk& x, int bc, float inv_bt,
                           f32x4 (&h1)[2], f32x4& z, f32x4& zb, f32x4 (&h3)[2], f32x4 (&y)[2], float& norm_c,
                           double& lacc) {
