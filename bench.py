@@ -49,6 +49,11 @@ def main(argv=None):
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--clients-per-gpu", type=int, default=10)
+    p.add_argument("--clients", type=int, default=None,
+                   help="fixed federation size (strong scaling, e.g. the paper's 10 clients on 8 GPUs); "
+                        "default: clients-per-gpu x GPUs (weak scaling)")
+    p.add_argument("--lr", type=float, default=1e-3)
+    p.add_argument("--shrink-lambda", type=float, default=5.0)
     p.add_argument("--epochs", type=int, default=5)
     p.add_argument("--batch-size", type=int, default=12)
     p.add_argument("--model-type", default="hybrid")
@@ -78,8 +83,9 @@ def main(argv=None):
         print(f"note: --gpus {args.gpus} but world size is {n_gpus}; using the world size", file=sys.stderr)
     out_root = tempfile.mkdtemp(prefix="fedmx_bench_") if comm.is_root else tempfile.mkdtemp(prefix="fedmx_bench_r")
     cfg = ExperimentConfig(
-        num_participants=0.5, epoch=args.epochs, num_rounds=10 ** 9, lr_rate=1e-3, shrink_lambda=5,
-        network_size=args.clients_per_gpu * n_gpus, batch_size=args.batch_size,
+        num_participants=0.5, epoch=args.epochs, num_rounds=10 ** 9, lr_rate=args.lr,
+        shrink_lambda=args.shrink_lambda,
+        network_size=args.clients if args.clients else args.clients_per_gpu * n_gpus, batch_size=args.batch_size,
         model_types=[args.model_type], update_types=[args.update_type],
         synthetic=args.data_kind, synthetic_iid=not args.non_iid, compat=args.compat, backend=args.backend,
         global_early_stop=False, save_checkpoints=not args.no_artifacts, output_root=out_root,
@@ -139,7 +145,7 @@ def main(argv=None):
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * dt / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.clients else "weak",
             "vs_baseline": round(value / BASELINE_ROUNDS_PER_SEC, 2),
             "dtype": "fp32",
             "data": (f"synthetic ({'N-BaIoT' if args.data_kind == 'nbaiot' else 'Kitsune'}-shaped, 115 features, "
@@ -147,7 +153,7 @@ def main(argv=None):
                      "random-init weights"),
             "config": {
                 "model": f"SAE 115-27-7-27-115 ({args.model_type}, {args.update_type}), "
-                         f"{args.clients_per_gpu} clients/GPU",
+                         + (f"{args.clients} clients" if args.clients else f"{args.clients_per_gpu} clients/GPU"),
                 "global_batch": args.batch_size,
                 "seq_len": 115,
                 "parallelism": f"client-sharded x{n_gpus} (RCCL all-gather/all-reduce)",
