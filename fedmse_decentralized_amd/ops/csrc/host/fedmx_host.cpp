@@ -159,8 +159,11 @@ int64_t fedmx_csv_parse(const char* path, double* out, int64_t rows, int64_t col
 }
 
 // Exact ROC-AUC (sklearn roc_curve+auc semantics: positives = label!=0,
-// ties count 1/2).  Returns NaN if a class is empty.
+// ties count 1/2).  Returns NaN if a class is empty or a score is NaN (sklearn
+// rejects NaN input; a NaN would also break the sort's strict weak ordering).
 double fedmx_roc_auc(const double* score, const int64_t* label, int64_t n) {
+  for (int64_t i = 0; i < n; ++i)
+    if (score[i] != score[i]) return __builtin_nan("");
   std::vector<int64_t> idx(n);
   std::iota(idx.begin(), idx.end(), 0);
   std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return score[a] < score[b]; });

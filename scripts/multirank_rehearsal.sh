@@ -1,5 +1,6 @@
 #!/bin/bash
-# Multi-rank rehearsal of bench.py / main.py on a ONE-GPU box: 2 ranks share
+# Multi-rank rehearsal of bench.py / main.py on a ONE-GPU box: NRANKS ranks
+# (default 2, at most 8 here) share
 # cuda:0 over the gloo backend (RCCL refuses duplicate GPUs).  Exercises the
 # sharded federation, the device-resident protocol's collectives and the
 # bench JSON contract (max over ranks) end to end.
@@ -7,16 +8,18 @@ set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
+NR=${NRANKS:-2}
+[ "$NR" -ge 2 ] && [ "$NR" -le 8 ] || { echo "NRANKS must be 2..8"; exit 2; }
 export FEDMX_DEVICE_INDEX=0 FEDMX_DIST_BACKEND=gloo HSA_ENABLE_IPC_MODE_LEGACY=0
 python -c "import fedmse_decentralized_amd.ops.build as b; b.build_all()" || exit 3
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-  --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 > "$OUT/rehearsal_bench2.log" 2>&1
+timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $NR --master-addr 127.0.0.1 \
+  --master-port 29517 bench.py --gpus $NR --steps 10 --warmup 2 > "$OUT/rehearsal_bench$NR.log" 2>&1
 rc=$?
-echo "bench 2 ranks rc=$rc"; tail -n 3 "$OUT/rehearsal_bench2.log"
+echo "bench $NR ranks rc=$rc"; tail -n 3 "$OUT/rehearsal_bench$NR.log"
 [ $rc -ne 0 ] && exit $rc
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $NR --master-addr 127.0.0.1 \
   --master-port 29518 main.py --synthetic nbaiot --num-rounds 2 --epoch 1 --model-types hybrid \
-  --update-types mse_avg --compat fixed --output-root "$OUT/rehearsal_main" --log-level WARNING > "$OUT/rehearsal_main2.log" 2>&1
+  --update-types mse_avg --compat fixed --output-root "$OUT/rehearsal_main" --log-level WARNING > "$OUT/rehearsal_main$NR.log" 2>&1
 rc=$?
-echo "main 2 ranks rc=$rc"; tail -n 3 "$OUT/rehearsal_main2.log"
+echo "main $NR ranks rc=$rc"; tail -n 3 "$OUT/rehearsal_main$NR.log"
 exit $rc

@@ -121,13 +121,15 @@ def _worker(rank, world, port, out):
 
 
 @pytest.mark.timeout(600)
-def test_device_round_two_ranks_one_gpu(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_device_round_multi_rank_one_gpu(tmp_path, world):
+    """world=4 shards 6 clients unevenly (2/2/1/1) over four gloo ranks."""
     out = str(tmp_path)
-    mp.start_processes(_worker, args=(2, _port(), out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _port(), out), nprocs=world, join=True, start_method="spawn")
     _shrink()
     fed, ref = _run(_cfg(os.path.join(out, "single"), save_checkpoints=False), "mse_avg", 4)
     ref_params = fed.engine.store.params.double().sum(1).tolist()
-    for r in range(2):
+    for r in range(world):
         d = json.load(open(os.path.join(out, f"rank{r}.json")))
         assert d["fast"]
         assert d["agg"] == ref["agg"] and d["sel"] == ref["sel"] and d["ver"] == ref["ver"]
