@@ -32,6 +32,11 @@ _lock = threading.Lock()
 # (fedmx_train8.hip, batch <= 16) — 1.62 ms vs 1.39 ms per 5-client x 5-epoch
 # launch on MI355X (profiles/r1_train8_stamps.txt)
 TRAIN_WAVES = int(os.environ.get("FEDMX_TRAIN_WAVES", "4"))
+# compact internal order of the 4-wave kernel (batch <= 12, hidden <= 27,
+# latent <= 7: padded k-steps skipped); FEDMX_TRAIN_COMPACT=0 forces the
+# identity order (A/B timing, cross-checks)
+TRAIN_COMPACT = os.environ.get("FEDMX_TRAIN_COMPACT", "1") != "0"
+TRAIN_FLAG_NO_COMPACT = 1
 _lib = None
 
 FWD_DTYPE = np.dtype([
@@ -64,7 +69,7 @@ class TrainArgs(ctypes.Structure):
         ("d_in", ctypes.c_int32), ("hidden", ctypes.c_int32), ("latent", ctypes.c_int32),
         ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
         ("eps", ctypes.c_float), ("lam", ctypes.c_float), ("mu", ctypes.c_float),
-        ("stamps", ctypes.c_void_p),
+        ("stamps", ctypes.c_void_p), ("flags", ctypes.c_int32), ("pad0", ctypes.c_int32),
     ]
 
 
@@ -458,7 +463,8 @@ class TrainBuffers:
         self.valid_off = torch.from_numpy(store.valid_off).to(dev)
 
 
-def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tensor] = None, waves: int = 0):
+def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tensor] = None, waves: int = 0,
+          compact: Optional[bool] = None):
     """Launch the fused training kernel for store rows ``local_ids`` (async).
     Returns host views (tracking[k, E, 2], epochs_run[k], best_epoch[k])
     written by the kernel, valid after the next stream sync."""
@@ -495,6 +501,7 @@ def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tens
     a.lr, a.beta1, a.beta2, a.eps = hp.lr, hp.beta1, hp.beta2, hp.eps
     a.lam, a.mu = hp.shrink_lambda, hp.fedprox_mu
     a.stamps = stamps.data_ptr() if stamps is not None else None
+    a.flags = 0 if (TRAIN_COMPACT if compact is None else compact) else TRAIN_FLAG_NO_COMPACT
     # the 8-wave variant covers single-tile batches only
     if hp.batch_size <= 16 and (waves or TRAIN_WAVES) == 8:
         rc = lib().fedmx_train8(ctypes.byref(a), k, rt.stream)

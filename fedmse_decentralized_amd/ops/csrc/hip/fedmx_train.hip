@@ -141,8 +141,16 @@ struct XChunk {
 // ONE: every batch is a single 16-row tile (batch <= 16, the reference's 12):
 // the per-chunk bookkeeping folds away and each step is one basic block the
 // scheduler can interleave (W4's optimizer VALU under the backward MFMAs).
-template <bool PROX, bool ONE>
+// CP (compact, implies ONE): batch <= 12, hidden <= 27, latent <= 7 — the
+// internal hidden / latent / batch orders of fedmx_train_common.h put every
+// padded slot into whole k-steps, which the products over hidden (7 of 8
+// k-steps), latent (2 of 4) and batch (3 of 4) skip: 95 instead of 116
+// MFMAs per wave and training step, and shorter dependent chains.
+template <bool PROX, bool ONE, bool CP>
 __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
+  static_assert(ONE || !CP, "compact order needs single-tile batches");
+  constexpr int KB = CP ? 3 : 4;   // k-steps of products over the batch
+  constexpr int KZ = CP ? 2 : 4;   // k-steps of products over the latent axis
   __shared__ __attribute__((aligned(16))) float lds[L_TOTAL];
   const int w = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -192,21 +200,21 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   // ---- load client state: global -> LDS masters -> owned registers ----------
   STAMP(true, 28);
   Slab P, M, V, AN;
-  global_to_masters(Mg, sW1, sW4, sW2, sW3);
+  global_to_masters_o<CP>(Mg, sW1, sW4, sW2, sW3);
   __syncthreads();
   lds_to_slab(M, L);
   __syncthreads();
-  global_to_masters(Vg, sW1, sW4, sW2, sW3);
+  global_to_masters_o<CP>(Vg, sW1, sW4, sW2, sW3);
   __syncthreads();
   lds_to_slab(V, L);
   __syncthreads();
   if (PROX) {
-    global_to_masters(A.anchor + (size_t)cid * P_PAD, sW1, sW4, sW2, sW3);
+    global_to_masters_o<CP>(A.anchor + (size_t)cid * P_PAD, sW1, sW4, sW2, sW3);
     __syncthreads();
     lds_to_slab(AN, L);
     __syncthreads();
   }
-  global_to_masters(Pg, sW1, sW4, sW2, sW3);
+  global_to_masters_o<CP>(Pg, sW1, sW4, sW2, sW3);
   __syncthreads();
   lds_to_slab(P, L);   // W2/W3/W4 masters stay live; W1 lives in registers only
   STAMP(true, 29);
@@ -232,6 +240,30 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
     fm0[r] = (xcol + r < d_in) ? 1.f : 0.f;
     fm1[r] = (xcol + 16 + r < d_in) ? 1.f : 0.f;
   }
+  // hidden / latent positions of this lane's D-layout registers (16t + 4g + r,
+  // 4g + r) and of its batch-major column (16t + c): real / bias flags
+  bool hreal_d[2][4], hbias_d[2][4], zreal_d[4], zbias_d[4], hreal_c[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = hslot_of_pos<CP>(16 * t + 4 * g + r);
+      hreal_d[t][r] = j < hidden;
+      hbias_d[t][r] = j == h_bias_slot<CP>();
+    }
+    hreal_c[t] = hslot_of_pos<CP>(16 * t + c) < hidden;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = zslot_of_pos<CP>(4 * g + r);
+    zreal_d[r] = j < latent;
+    zbias_d[r] = j == z_bias_slot<CP>();
+  }
+  // batch rows of this lane's tile column c and batch-major rows 4g + r (-1: padding)
+  const int brow_c = batch_row_of_col<CP>(c);
+  int brow_b[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) brow_b[r] = batch_row_of_col<CP>(4 * g + r);
   bool stamp_fwd = false;
   (void)stamp_fwd;
 
@@ -240,22 +272,22 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   // applied by finalize_chunk when the chunk is consumed, so issuing the
   // loads never waits for them.
   auto load_chunk = [&](const float* X, int row0, int bc, XChunk& x) {
-    const float* src = X + (size_t)(row0 + (c < bc ? c : 0)) * DP + xcol;
+    const float* src = X + (size_t)(row0 + ((unsigned)brow_c < (unsigned)bc ? brow_c : 0)) * DP + xcol;
     x.f0 = *reinterpret_cast<const f32x4*>(src);
     x.f1 = *reinterpret_cast<const f32x4*>(src + 16);
     const float* bsrc = X + (size_t)row0 * DP + 32 * w + c;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int rr = (4 * g + r < bc) ? 4 * g + r : 0;
+      const int rr = ((unsigned)brow_b[r] < (unsigned)bc) ? brow_b[r] : 0;
       x.b0[r] = bsrc[(size_t)rr * DP];
       x.b1[r] = bsrc[(size_t)rr * DP + 16];
     }
   };
   auto finalize_chunk = [&](int bc, XChunk& x) {
-    const bool ok = c < bc;
+    const bool ok = (unsigned)brow_c < (unsigned)bc;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const bool okr = 4 * g + r < bc;
+      const bool okr = (unsigned)brow_b[r] < (unsigned)bc;
       x.f0[r] = ok ? x.f0[r] : 0.f;
       x.f1[r] = ok ? x.f1[r] : 0.f;
       x.b0[r] = okr ? x.b0[r] : 0.f;
@@ -264,8 +296,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
     if (bias_lane) x.f1[3] = 1.f;
   };
   auto load_chunk_f = [&](const float* X, int row0, int bc, XChunk& x) {  // validation: feature-major only
-    const bool ok = c < bc;
-    const float* src = X + (size_t)(row0 + (ok ? c : 0)) * DP + xcol;
+    const bool ok = (unsigned)brow_c < (unsigned)bc;
+    const float* src = X + (size_t)(row0 + (ok ? brow_c : 0)) * DP + xcol;
     const f32x4 f0 = *reinterpret_cast<const f32x4*>(src);
     const f32x4 f1 = *reinterpret_cast<const f32x4*>(src + 16);
 #pragma unroll
@@ -322,7 +354,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float vv = fmaxf(s[r], 0.f);
-        if (16 * t + 4 * g + r == HP - 1) vv = 1.f;
+        if (hbias_d[t][r]) vv = 1.f;
         s[r] = vv;
       }
       h1[t] = s;
@@ -335,23 +367,26 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) z = mfma16(a0[s], h1[0][s], z);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) z = mfma16(a1[s], h1[1][s], z);
+      for (int s = 0; s < (CP ? 3 : 4); ++s) z = mfma16(a1[s], h1[1][s], z);
     }
     zb = z;
-    if (g == 3) zb[3] = 1.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (zbias_d[r]) zb[r] = 1.f;
     {
       f32x4 acc0 = zero4(), acc1 = zero4();
       const f32x4 a0 = lds_read4(a3p);
       const f32x4 a1 = lds_read4(a3p + 16 * S_W3);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
+      for (int s = 0; s < KZ; ++s) {
         acc0 = mfma16(a0[s], zb[s], acc0);
         acc1 = mfma16(a1[s], zb[s], acc1);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v0 = fmaxf(acc0[r], 0.f), v1 = fmaxf(acc1[r], 0.f);
-        if (16 + 4 * g + r == HP - 1) v1 = 1.f;
+        if (hbias_d[0][r]) v0 = 1.f;
+        if (hbias_d[1][r]) v1 = 1.f;
         acc0[r] = v0;
         acc1[r] = v1;
       }
@@ -370,7 +405,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         acc1 = mfma16(a10[s], h3[0][s], acc1);
       }
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
+      for (int s = 0; s < (CP ? 3 : 4); ++s) {
         acc0 = mfma16(a01[s], h3[1][s], acc0);
         acc1 = mfma16(a11[s], h3[1][s], acc1);
       }
@@ -384,14 +419,15 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       const float d1 = (y[1][r] - x.f1[r]) * fm1[r];
       sq += d0 * d0 + d1 * d1;
     }
-    sq = (c < bc) ? sq : 0.f;
+    const bool col_ok = (unsigned)brow_c < (unsigned)bc;
+    sq = col_ok ? sq : 0.f;
     float nz = 0.f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) nz += (4 * g + r < latent) ? z[r] * z[r] : 0.f;
+    for (int r = 0; r < 4; ++r) nz += zreal_d[r] ? z[r] * z[r] : 0.f;
     nz = sum_lane_groups(nz);
     norm_c = __builtin_amdgcn_sqrtf(nz);
     float contrib = sq * (inv_bt * inv_d);
-    if (w == 0 && g == 0 && c < bc) contrib += lam * norm_c * inv_bt;
+    if (w == 0 && g == 0 && col_ok) contrib += lam * norm_c * inv_bt;
     lacc += (double)contrib;
   };
 
@@ -468,7 +504,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         }
 
       // ---- dY (masked, feature-major) and the transposes feeding dW4
-      const float scale = (c < bc) ? 2.0f / (float)(bt * d_in) : 0.f;
+      const bool col_ok = (unsigned)brow_c < (unsigned)bc;
+      const float scale = col_ok ? 2.0f / (float)(bt * d_in) : 0.f;
       f32x4 dy[2];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -508,7 +545,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         const f32x4 b0 = lds_read4(sT1 + tr);
         const f32x4 b1 = lds_read4(sT1 + tr + 16 * S_T);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+        for (int s = 0; s < KB; ++s) {
           G4[0][0] = mfma16(a0[s], b0[s], G4[0][0]);
           G4[0][1] = mfma16(a0[s], b1[s], G4[0][1]);
           G4[1][0] = mfma16(a1[s], b0[s], G4[1][0]);
@@ -531,8 +568,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int h = 16 * t + 4 * g + r;
-          s[r] = (h < hidden && h3[t][r] > 0.f) ? s[r] : 0.f;
+          s[r] = (hreal_d[t][r] && h3[t][r] > 0.f) ? s[r] : 0.f;
         }
         dh3[t] = s;
       }
@@ -565,13 +601,13 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       //      lambda/B * z / ||z|| (0 where ||z|| == 0)
       f32x4 dz = zero4();
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int s = 0; s < 4; ++s) dz = mfma16(q3[0][s], dh3[0][s], dz);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) dz = mfma16(q3[t][s], dh3[t][s], dz);
+      for (int s = 0; s < (CP ? 3 : 4); ++s) dz = mfma16(q3[1][s], dh3[1][s], dz);
       const float shr_raw = lam * __builtin_amdgcn_rcpf((float)bt * norm_c);
-      const float shr = (c < bc && norm_c > 0.f) ? shr_raw : 0.f;
+      const float shr = (col_ok && norm_c > 0.f) ? shr_raw : 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dz[r] = (4 * g + r < latent) ? dz[r] + shr * z[r] : 0.f;
+      for (int r = 0; r < 4; ++r) dz[r] = zreal_d[r] ? dz[r] + shr * z[r] : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) sDZT[tw + r * S_T] = dz[r];
       // ---- dH1 in the batch-major layout, D[b=4g+r][h=16t+c] = sum_z dZ[b][z] W2a[z][h]
@@ -583,15 +619,15 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         h1b[t] = lds_read4(sH1T + tr + 16 * t * S_T);
         f32x4 acc = zero4();
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma16(dz[s], q2[t][s], acc);
+        for (int s = 0; s < KZ; ++s) acc = mfma16(dz[s], q2[t][s], acc);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = (16 * t + c < hidden && h1b[t][r] > 0.f) ? acc[r] : 0.f;
+        for (int r = 0; r < 4; ++r) acc[r] = (hreal_c[t] && h1b[t][r] > 0.f) ? acc[r] : 0.f;
         dh1b[t] = acc;
       }
       STAMP(stamp_on, 8);
       // ---- dW1^T (own columns) = X^T dH1: D[d=4g+r][h=c] lands in the q1 layout
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
+      for (int s = 0; s < KB; ++s) {
         G1[0][0] = mfma16(cur.b0[s], dh1b[0][s], G1[0][0]);
         G1[0][1] = mfma16(cur.b1[s], dh1b[0][s], G1[0][1]);
         G1[1][0] = mfma16(cur.b0[s], dh1b[1][s], G1[1][0]);
@@ -605,7 +641,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         const f32x4 bz = lds_read4(sZT + tr);
         const f32x4 b = (w < 2) ? bz : ((w == 2) ? h1b[0] : h1b[1]);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) Go = mfma16(a[s], b[s], Go);
+        for (int s = 0; s < KB; ++s) Go = mfma16(a[s], b[s], Go);
       }
       STAMP(stamp_on, 9);
       if (last) {
@@ -717,7 +753,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       min_valid = valid_loss;
       best_ep = ep;
       worse = 0;
-      masters_to_global(Bg, sW1, sW4, sW2, sW3);  // save_model(): best-validation snapshot
+      masters_to_global_o<CP>(Bg, sW1, sW4, sW2, sW3);  // save_model(): best-validation snapshot
     } else {
       ++worse;
     }
@@ -730,15 +766,15 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   // ---- write back: params (masters), then m and v through the same staging
   w1_to_lds(P, L);
   __syncthreads();
-  masters_to_global(Pg, sW1, sW4, sW2, sW3);
+  masters_to_global_o<CP>(Pg, sW1, sW4, sW2, sW3);
   __syncthreads();
   slab_to_lds(M, L);
   __syncthreads();
-  masters_to_global(Mg, sW1, sW4, sW2, sW3);
+  masters_to_global_o<CP>(Mg, sW1, sW4, sW2, sW3);
   __syncthreads();
   slab_to_lds(V, L);
   __syncthreads();
-  masters_to_global(Vg, sW1, sW4, sW2, sW3);
+  masters_to_global_o<CP>(Vg, sW1, sW4, sW2, sW3);
   if (threadIdx.x == 0) {
     A.adam_step[cid] = step;
     A.epochs_run[kslot] = ep_run;
@@ -759,16 +795,21 @@ int fedmx_train(const void* args, int k, hipStream_t stream) {
       A.latent > fedmx::ZP - 1)
     return -3;
   const bool one = A.batch <= 16;
+  const bool cp = A.batch <= 12 && A.hidden <= 27 && A.latent <= 7 && !(A.flags & fedmx::TRAIN_FLAG_NO_COMPACT);
   if (A.mu != 0.f) {
-    if (one)
-      hipLaunchKernelGGL((fedmx::train_kernel<true, true>), dim3(k), dim3(256), 0, stream, A);
+    if (cp)
+      hipLaunchKernelGGL((fedmx::train_kernel<true, true, true>), dim3(k), dim3(256), 0, stream, A);
+    else if (one)
+      hipLaunchKernelGGL((fedmx::train_kernel<true, true, false>), dim3(k), dim3(256), 0, stream, A);
     else
-      hipLaunchKernelGGL((fedmx::train_kernel<true, false>), dim3(k), dim3(256), 0, stream, A);
+      hipLaunchKernelGGL((fedmx::train_kernel<true, false, false>), dim3(k), dim3(256), 0, stream, A);
   } else {
-    if (one)
-      hipLaunchKernelGGL((fedmx::train_kernel<false, true>), dim3(k), dim3(256), 0, stream, A);
+    if (cp)
+      hipLaunchKernelGGL((fedmx::train_kernel<false, true, true>), dim3(k), dim3(256), 0, stream, A);
+    else if (one)
+      hipLaunchKernelGGL((fedmx::train_kernel<false, true, false>), dim3(k), dim3(256), 0, stream, A);
     else
-      hipLaunchKernelGGL((fedmx::train_kernel<false, false>), dim3(k), dim3(256), 0, stream, A);
+      hipLaunchKernelGGL((fedmx::train_kernel<false, false, false>), dim3(k), dim3(256), 0, stream, A);
   }
   return (int)hipGetLastError();
 }

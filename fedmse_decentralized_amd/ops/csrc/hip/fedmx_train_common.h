@@ -28,7 +28,10 @@ struct TrainArgs {
   int32_t epochs, batch, patience, d_in, hidden, latent;
   float lr, beta1, beta2, eps, lambda, mu;
   uint64_t* stamps;         // [4 waves][32] s_memtime stamps of one step (FEDMX_STAMPS builds), or null
+  int32_t flags;            // TRAIN_FLAG_* bits
+  int32_t pad0;
 };
+constexpr int32_t TRAIN_FLAG_NO_COMPACT = 1;  // identity-order kernels even where the compact order applies
 
 // In-kernel phase timestamps (build with -DFEDMX_STAMPS=1): wave w's lane 0 of
 // workgroup 0 records s_memtime at fixed points of training step STAMP_STEP
@@ -170,5 +173,106 @@ __device__ __forceinline__ void masters_to_global(float* __restrict__ dst, const
   }
 }
 
+
+// ---- compact internal order (train_kernel<.., CP = true>) --------------------
+// For the reference shapes (hidden <= 27, latent <= 7, batch <= 12) the kernel
+// keeps the hidden and latent axes of its LDS masters / register tiles in a
+// permuted order in which every padded slot falls into whole MFMA k-steps, so
+// contractions over hidden, latent and batch skip those k-steps:
+//   hidden: storage index h -> slot j (h < 27: j = h; bias h = HP-1: j = 27;
+//           pads 27..30: j = 28..31) -> position 16(ks>>2) + 4(j&3) + (ks&3),
+//           ks = j>>2; slots 28..31 are exactly k-step (t=1, s=3).
+//   latent: storage z -> slot j (z < 7: j = z; bias: 7; pads: 8..15) ->
+//           position 4(j&3) + (j>>2); slots 0..7 are k-steps s = 0, 1.
+//   batch : tile column (lane) p holds batch row 3(p>>2) + (p&3) for p&3 < 3;
+//           columns 3, 7, 11, 15 (= k-step s = 3 of every product that sums
+//           over the batch) are always padding.
+// CP = false is the identity order (position = storage index, lane = row).
+template <bool CP>
+__device__ __forceinline__ int hslot_of_pos(int p) {
+  return CP ? 16 * (p >> 4) + 4 * (p & 3) + ((p >> 2) & 3) : p;
+}
+template <bool CP>
+__device__ __forceinline__ int hpos_of_storage(int h) {
+  if (!CP) return h;
+  const int j = h < 27 ? h : (h == HP - 1 ? 27 : h + 1);
+  const int ks = j >> 2;
+  return 16 * (ks >> 2) + 4 * (j & 3) + (ks & 3);
+}
+template <bool CP>
+__device__ __forceinline__ int zslot_of_pos(int p) {
+  return CP ? 4 * (p & 3) + (p >> 2) : p;
+}
+template <bool CP>
+__device__ __forceinline__ int zpos_of_storage(int z) {
+  if (!CP) return z;
+  const int j = z < 7 ? z : (z == ZP - 1 ? 7 : z + 1);
+  return 4 * (j & 3) + (j >> 2);
+}
+template <bool CP>
+constexpr int h_bias_slot() { return CP ? 27 : HP - 1; }
+template <bool CP>
+constexpr int z_bias_slot() { return CP ? 7 : ZP - 1; }
+// batch row held by tile column p, or -1 for a padding column
+template <bool CP>
+__device__ __forceinline__ int batch_row_of_col(int p) {
+  return CP ? ((p & 3) == 3 ? -1 : 3 * (p >> 2) + (p & 3)) : p;
+}
+
+// dense global [P_PAD] (storage order) <-> LDS masters (internal order)
+template <bool CP>
+__device__ __forceinline__ void global_to_masters_o(const float* __restrict__ src, float* sW1, float* sW4,
+                                                    float* sW2, float* sW3) {
+  if (!CP) {
+    global_to_masters(src, sW1, sW4, sW2, sW3);
+    return;
+  }
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
+  for (int i = threadIdx.x; i < OFF_W2 / 4; i += blockDim.x) {  // W1a rows permuted
+    const int e = i * 4;
+    lds_write4(&sW1[hpos_of_storage<true>(e / DP) * S_W1 + (e % DP)], s4[i]);
+  }
+  for (int e = OFF_W2 + threadIdx.x; e < P_PAD; e += blockDim.x) {
+    const float val = src[e];
+    if (e < OFF_W3) {
+      const int q = e - OFF_W2;
+      sW2[zpos_of_storage<true>(q / HP) * S_W2 + hpos_of_storage<true>(q % HP)] = val;
+    } else if (e < OFF_W4) {
+      const int q = e - OFF_W3;
+      sW3[hpos_of_storage<true>(q / ZP) * S_W3 + zpos_of_storage<true>(q % ZP)] = val;
+    } else {
+      const int q = e - OFF_W4;
+      sW4[(q / HP) * S_W4 + hpos_of_storage<true>(q % HP)] = val;
+    }
+  }
+}
+
+template <bool CP>
+__device__ __forceinline__ void masters_to_global_o(float* __restrict__ dst, const float* sW1, const float* sW4,
+                                                    const float* sW2, const float* sW3) {
+  if (!CP) {
+    masters_to_global(dst, sW1, sW4, sW2, sW3);
+    return;
+  }
+  f32x4* d4 = reinterpret_cast<f32x4*>(dst);
+  for (int i = threadIdx.x; i < OFF_W2 / 4; i += blockDim.x) {
+    const int e = i * 4;
+    d4[i] = lds_read4(&sW1[hpos_of_storage<true>(e / DP) * S_W1 + (e % DP)]);
+  }
+  for (int e = OFF_W2 + threadIdx.x; e < P_PAD; e += blockDim.x) {
+    float val;
+    if (e < OFF_W3) {
+      const int q = e - OFF_W2;
+      val = sW2[zpos_of_storage<true>(q / HP) * S_W2 + hpos_of_storage<true>(q % HP)];
+    } else if (e < OFF_W4) {
+      const int q = e - OFF_W3;
+      val = sW3[hpos_of_storage<true>(q / ZP) * S_W3 + zpos_of_storage<true>(q % ZP)];
+    } else {
+      const int q = e - OFF_W4;
+      val = sW4[(q / HP) * S_W4 + hpos_of_storage<true>(q % HP)];
+    }
+    dst[e] = val;
+  }
+}
 
 }  // namespace fedmx

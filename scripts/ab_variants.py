@@ -1,0 +1,39 @@
+"""Build variants of the HIP library for A/B timing of the training kernel.
+
+    python scripts/ab_variants.py build            # on the CPU host (hipcc cross-compiles)
+    bash scripts/ab_train.sh                       # on the GPU box: times every built variant
+
+Each variant is ``libfedmx_hip_<name>.so`` next to the main library, built
+with the extra compiler flags below; ``scripts/ab_train.sh`` loads each one
+through ``FEDMX_HIP_LIB`` in its own process.
+"""
+from __future__ import annotations
+
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from fedmse_decentralized_amd.ops import build  # noqa: E402
+
+VARIANTS = {
+    "base": [],
+    "noslp": ["-fno-slp-vectorize"],
+    "noslp_nohint": ["-fno-slp-vectorize", "-DFEDMX_SCHED_HINTS=0"],
+    "nohint": ["-DFEDMX_SCHED_HINTS=0"],
+}
+
+
+def main():
+    names = sys.argv[2:] or list(VARIANTS)
+    if sys.argv[1:2] == ["build"]:
+        for n in names:
+            t = build.LIBDIR / f"libfedmx_hip_{n}.so"
+            build.build_hip(force=True, extra_flags=VARIANTS[n], target=t)
+            print("built", t)
+    elif sys.argv[1:2] == ["list"]:
+        print(" ".join(names))
+
+
+if __name__ == "__main__":
+    main()

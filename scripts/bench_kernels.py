@@ -49,6 +49,7 @@ def main():
     p.add_argument("--clients", type=int, default=10)
     p.add_argument("--train-clients", type=int, default=5)
     p.add_argument("--reps", type=int, default=20)
+    p.add_argument("--train-only", action="store_true", help="only the training-kernel timings (A/B of builds)")
     args = p.parse_args()
     dev = torch.device("cuda", 0)
     raws = generate_federation(SyntheticSpec(kind="nbaiot", n_clients=args.clients, seed=1))
@@ -77,6 +78,12 @@ def main():
     hpp = TrainHParams(epochs=args.epochs, batch_size=12, lr=1e-3, shrink_lambda=5.0, fedprox_mu=0.001,
                        patience=10 ** 6)
     out["train_launch_fedprox_us"] = timeit(lambda: eng.train_async(sel, hpp), reps=args.reps)[0]
+    _hip.TRAIN_COMPACT = False   # identity internal order (no padded k-steps skipped)
+    out["train_launch_identity_order_us"] = timeit(lambda: eng.train_async(sel, hp), reps=args.reps)[0]
+    _hip.TRAIN_COMPACT = True
+    if args.train_only:
+        print(json.dumps({k: round(v, 3) if isinstance(v, float) else v for k, v in out.items()}))
+        return
     allc = list(range(args.clients))
     items = [(c, eng.store.rows("test", c)) for c in allc]
     out["fwd_sse_all_test_us"] = timeit(lambda: eng.forward_rows(eng.store.params, items, True, False))[0]

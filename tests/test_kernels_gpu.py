@@ -143,6 +143,34 @@ def test_train_kernel_matches_torch_engine(lam, mu, batch):
     assert torch.count_nonzero(hip.store.params[:, pad]) == 0
 
 
+@pytest.mark.parametrize("batch,lam,mu", [(12, 5.0, 0.0), (7, 1.0, 0.001), (1, 5.0, 0.0), (12, 0.0, 0.01)])
+def test_train_kernel_compact_order_matches_identity_order(batch, lam, mu):
+    """The compact internal order (padded hidden / latent / batch k-steps
+    skipped) computes the same training as the identity order up to fp32
+    summation order."""
+    from fedmse_decentralized_amd.models.layout import real_mask_padded
+
+    _, a = _setup_pair(seed=11)
+    _, b = _setup_pair(seed=11)
+    anchor = a.store.params + 0.01 * torch.randn(a.store.params.shape, generator=torch.Generator().manual_seed(6),
+                                                 device="cpu").to(DEV)
+    anchor = canonical_to_padded(padded_to_canonical(anchor.cpu())).to(DEV)
+    a.store.anchor.copy_(anchor)
+    b.store.anchor.copy_(anchor)
+    hp = TrainHParams(epochs=3, batch_size=batch, lr=1e-3, shrink_lambda=lam, fedprox_mu=mu, patience=1)
+    ta, ea, ba = _hip.train(a.store, [0, 1], hp, a.dims, compact=True)
+    tb, eb, bb = _hip.train(b.store, [0, 1], hp, b.dims, compact=False)
+    torch.cuda.synchronize()
+    _hip.runtime(DEV).sync()
+    assert list(ea) == list(eb) and list(ba) == list(bb)
+    np.testing.assert_allclose(np.array(ta), np.array(tb), rtol=1e-5, atol=1e-7)
+    for name in ("params", "best", "adam_m", "adam_v"):
+        torch.testing.assert_close(getattr(a.store, name), getattr(b.store, name), rtol=1e-3, atol=1e-6)
+    pad = ~real_mask_padded().to(DEV)
+    for name in ("params", "best", "adam_m", "adam_v"):
+        assert torch.count_nonzero(getattr(a.store, name)[:, pad]) == 0
+
+
 def test_train_kernel_single_step_tight():
     # one Adam step from identical state: errors are pure fp32 rounding
     ref, hip = _setup_pair(n_train=(12,), n_valid=(12,), seed=3)
