@@ -40,8 +40,12 @@
 // columns and padded features are masked out of the loss and every gradient.
 #include "fedmx_train_common.h"
 
+// 0: compiler schedule; 1..3: sched_group_barrier MFMA/VALU interleaving
+// patterns; 4: iglp_opt(0) (fastest measured with the compact order and the
+// FMA-form Adam: 1.211 vs 1.231 ms compiler / 1.257 ms pattern 1 per
+// 5-client x 5-epoch launch); 5: iglp_opt(1)
 #ifndef FEDMX_SCHED_HINTS
-#define FEDMX_SCHED_HINTS 1
+#define FEDMX_SCHED_HINTS 4
 #endif
 
 namespace fedmx {
@@ -431,6 +435,138 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
     lacc += (double)contrib;
   };
 
+  // Whole forward of one validation chunk by this wave alone (see the
+  // validation pass): L1 as four K-block partials (wave-order sum), L2/L3 as
+  // in forward_rest, L4 for all 128 rows, loss shares per K-block.
+  auto valid_chunk = [&](const float* X, int row0, int bc, float inv_bt, double& lacc) {
+    // the masters are loop-invariant here; keep their reads inside the loop
+    // (hoisting ~40 b128 operand reads out of it would spill the Adam slabs)
+    asm volatile("" ::: "memory");
+    const bool ok = (unsigned)brow_c < (unsigned)bc;
+    const float* src = X + (size_t)(row0 + (ok ? brow_c : 0)) * DP + 4 * g;
+    f32x4 xf[4][2];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const f32x4 q = *reinterpret_cast<const f32x4*>(src + 32 * b + 16 * v);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xf[b][v][r] = ok ? q[r] : 0.f;
+      }
+    if (g == 3) xf[3][1][3] = 1.f;   // bias column DP-1
+    f32x4 h1[2];
+    {
+      // K-block partials one after another, each added to the running sum as
+      // soon as it is complete: ((p0 + p1) + p2) + p3 with two live chains
+      f32x4 sum0 = zero4(), sum1 = zero4();
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        f32x4 p0 = zero4(), p1 = zero4();
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const f32x4 a0 = lds_read4(sW1 + c * S_W1 + 32 * b + 16 * v + 4 * g);
+          const f32x4 a1 = lds_read4(sW1 + (16 + c) * S_W1 + 32 * b + 16 * v + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            p0 = mfma16(a0[r], xf[b][v][r], p0);
+            p1 = mfma16(a1[r], xf[b][v][r], p1);
+          }
+        }
+        if (b == 0) {
+          sum0 = p0;
+          sum1 = p1;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            sum0[r] = sum0[r] + p0[r];
+            sum1[r] = sum1[r] + p1[r];
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v0 = fmaxf(sum0[r], 0.f), v1 = fmaxf(sum1[r], 0.f);
+        if (hbias_d[0][r]) v0 = 1.f;
+        if (hbias_d[1][r]) v1 = 1.f;
+        sum0[r] = v0;
+        sum1[r] = v1;
+      }
+      h1[0] = sum0;
+      h1[1] = sum1;
+    }
+    f32x4 z = zero4();
+    {
+      const f32x4 a0 = lds_read4(a2p);
+      const f32x4 a1 = lds_read4(a2p + 16);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) z = mfma16(a0[s], h1[0][s], z);
+#pragma unroll
+      for (int s = 0; s < (CP ? 3 : 4); ++s) z = mfma16(a1[s], h1[1][s], z);
+    }
+    f32x4 zb = z;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (zbias_d[r]) zb[r] = 1.f;
+    f32x4 h3[2];
+    {
+      f32x4 acc0 = zero4(), acc1 = zero4();
+      const f32x4 a0 = lds_read4(a3p);
+      const f32x4 a1 = lds_read4(a3p + 16 * S_W3);
+#pragma unroll
+      for (int s = 0; s < KZ; ++s) {
+        acc0 = mfma16(a0[s], zb[s], acc0);
+        acc1 = mfma16(a1[s], zb[s], acc1);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v0 = fmaxf(acc0[r], 0.f), v1 = fmaxf(acc1[r], 0.f);
+        if (hbias_d[0][r]) v0 = 1.f;
+        if (hbias_d[1][r]) v1 = 1.f;
+        acc0[r] = v0;
+        acc1[r] = v1;
+      }
+      h3[0] = acc0;
+      h3[1] = acc1;
+    }
+    float nz = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) nz += zreal_d[r] ? z[r] * z[r] : 0.f;
+    nz = sum_lane_groups(nz);
+    const float norm_v = __builtin_amdgcn_sqrtf(nz);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      f32x4 acc0 = zero4(), acc1 = zero4();
+      const float* ap = sW4 + (32 * b + c) * S_W4 + 4 * g;
+      const f32x4 a00 = lds_read4(ap);
+      const f32x4 a01 = lds_read4(ap + 16);
+      const f32x4 a10 = lds_read4(ap + 16 * S_W4);
+      const f32x4 a11 = lds_read4(ap + 16 * S_W4 + 16);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc0 = mfma16(a00[s], h3[0][s], acc0);
+        acc1 = mfma16(a10[s], h3[0][s], acc1);
+      }
+#pragma unroll
+      for (int s = 0; s < (CP ? 3 : 4); ++s) {
+        acc0 = mfma16(a01[s], h3[1][s], acc0);
+        acc1 = mfma16(a11[s], h3[1][s], acc1);
+      }
+      float sq = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float m0 = (32 * b + 4 * g + r < d_in) ? 1.f : 0.f;
+        const float m1 = (32 * b + 16 + 4 * g + r < d_in) ? 1.f : 0.f;
+        const float d0 = (acc0[r] - xf[b][0][r]) * m0;
+        const float d1 = (acc1[r] - xf[b][1][r]) * m1;
+        sq += d0 * d0 + d1 * d1;
+      }
+      sq = ok ? sq : 0.f;
+      float contrib = sq * (inv_bt * inv_d);
+      if (b == 0 && g == 0 && ok) contrib += lam * norm_v * inv_bt;
+      lacc += (double)contrib;
+    }
+  };
+
   AdamStep K;
   K.one_m_b1 = 1.f - A.beta1;
   K.b2 = A.beta2;
@@ -665,11 +801,29 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
           // the scheduler to interleave the optimizer / mask VALU work into
           // the MFMA gaps (one wave per SIMD co-issues ~6 VALU per 16x16x4
           // MFMA) instead of running the two streams back to back.
+#if FEDMX_SCHED_HINTS == 1
 #pragma unroll
           for (int i = 0; i < 64; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
             __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // 6 VALU
           }
+#elif FEDMX_SCHED_HINTS == 2
+#pragma unroll
+          for (int i = 0; i < 48; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+          }
+#elif FEDMX_SCHED_HINTS == 3
+#pragma unroll
+          for (int i = 0; i < 48; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);
+          }
+#elif FEDMX_SCHED_HINTS == 4
+          __builtin_amdgcn_iglp_opt(0);
+#elif FEDMX_SCHED_HINTS == 5
+          __builtin_amdgcn_iglp_opt(1);
+#endif
         }
 #endif
       } else {
@@ -682,26 +836,29 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       ch = ch_n;
     }
 
-    // ---- validation pass (eval mode, no grad)
+    // ---- validation pass (eval mode, no grad).  The waves split the batches
+    // (wave w: batches w, w+4, ...) and each runs a whole forward from the
+    // LDS masters: no cross-wave reduction, no barrier per batch.  Layer 1 is
+    // still summed as the training step's four K-block partials in wave
+    // order and each K-block's loss share is formed as there, so every
+    // per-lane fp32 loss contribution is bitwise the one the training-step
+    // forward would produce.
+    STAMP(ep == 0, 14);
+    w1_to_lds(P, L);   // W1 master (also the source of a best-validation snapshot)
+    __syncthreads();   // every wave's owned rows / tiles published
     double acc_va = 0.0;
-    for (int vb = 0; vb < nvb; ++vb) {
+    for (int vb = w; vb < nvb; vb += 4) {
       const int row0 = vb * B;
       const int bt = min(B, n_va - row0);
       const float inv_bt = 1.0f / (float)bt;
       for (int c0 = 0; c0 < bt; c0 += 16) {
         const int bc = min(16, bt - c0);
-        XChunk xv;
-        STAMP(ep == 0 && vb == 1 && c0 == 0, 16);
-        load_chunk_f(Xva, row0 + c0, bc, xv);
-        f32x4 a0, a1;
-        l1_partial(xv, a0, a1);
-        f32x4 h1[2], z, zb, h3[2], y[2];
-        float norm_c;
-        STAMP(ep == 0 && vb == 1 && c0 == 0, 17);
-        forward_rest(a0, a1, xv, bc, inv_bt, h1, z, zb, h3, y, norm_c, acc_va);
-        STAMP(ep == 0 && vb == 1 && c0 == 0, 18);
+        STAMP(ep == 0 && vb == w && c0 == 0, 16);
+        valid_chunk(Xva, row0 + c0, bc, inv_bt, acc_va);
+        STAMP(ep == 0 && vb == w && c0 == 0, 17);
       }
     }
+    STAMP(ep == 0, 15);
     STAMP(ep == 0, 12);
     double prox_now = 0.0;
     if (PROX) {
@@ -723,8 +880,6 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       }
       prox_now = (double)pr;
     }
-    // W1 master for a possible best-validation snapshot (covered by the barrier below)
-    w1_to_lds(P, L);
     // ---- epoch-end reduction (fixed order over waves -> identical decision everywhere)
     {
       const double s0 = wave_sum_d(acc_tr);

@@ -17,10 +17,14 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from fedmse_decentralized_amd.ops import build  # noqa: E402
 
 VARIANTS = {
-    "base": [],
+    "base": [],                                   # defaults: FMA-form Adam, iglp_opt(0)
+    "sched0": ["-DFEDMX_SCHED_HINTS=0"],          # compiler schedule
     "noslp": ["-fno-slp-vectorize"],
-    "noslp_nohint": ["-fno-slp-vectorize", "-DFEDMX_SCHED_HINTS=0"],
-    "nohint": ["-DFEDMX_SCHED_HINTS=0"],
+    "sepadam": ["-DFEDMX_ADAM_FMA=0"],
+    "hint1": ["-DFEDMX_SCHED_HINTS=1"],           # 64 x (1 MFMA, 6 VALU)
+    "hint2": ["-DFEDMX_SCHED_HINTS=2"],           # 48 x (1 MFMA, 4 VALU)
+    "hint3": ["-DFEDMX_SCHED_HINTS=3"],           # 48 x (1 MFMA, 10 VALU)
+    "iglp1": ["-DFEDMX_SCHED_HINTS=5"],
 }
 
 

@@ -33,13 +33,14 @@ PHASES = [
     (3, 4, "prefetch + dY/transposes + dH3 partial + stage"), (4, 5, "dW4 mfma"),
     (6, 7, "barrier #2"), (7, 8, "dH3 reduce + dZ + dH1 (batch-major)"), (8, 9, "dW1 mfma + small tile"),
     (9, 10, "adam W1"), (10, 11, "next L1 + adam W4/small + publish"), (0, 11, "TRAIN STEP TOTAL"),
-    (16, 17, "valid: load chunk + L1"), (17, 18, "valid: forward rest"), (28, 29, "prologue (state load)"),
+    (16, 17, "valid: one chunk (one wave)"), (14, 15, "valid: epoch pass (per wave)"),
+    (28, 29, "prologue (state load)"),
     (12, 13, "epoch end (reduce + snapshot)"), (30, 31, "epilogue (write back)"),
 ]
 
 
 def main():
-    if not PLAIN:
+    if not PLAIN and not build.HIP_STAMPS_LIB.exists():
         build.build_hip(extra_flags=["-DFEDMX_STAMPS=1"], target=build.HIP_STAMPS_LIB)
     dev = torch.device("cuda", 0)
     raws = generate_federation(SyntheticSpec(kind="nbaiot", n_clients=10, seed=1))
