@@ -84,8 +84,12 @@ def build_hip(force: bool = False, verbose: bool = False, extra_flags=(), target
     tmp = target.with_suffix(".so.tmp")
     # -ffp-contract=off: separately rounded mul/add like the torch ops the kernels
     # reproduce (aggregation sums are then bit-identical to the reference order)
+    # -amdgpu-mfma-vgpr-form: MFMA accumulators in arch VGPRs (the training
+    # kernel otherwise pays ~150 v_accvgpr moves per step on its VALU-bound
+    # optimizer tail: -3.3% launch time measured)
     cmd = [hipcc_path(), f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-munsafe-fp-atomics", f"-I{CSRC / 'hip'}", *extra_flags, *map(str, srcs),
+           "-ffp-contract=off", "-munsafe-fp-atomics", "-mllvm", "-amdgpu-mfma-vgpr-form=1",
+           f"-I{CSRC / 'hip'}", *extra_flags, *map(str, srcs),
            "-o", str(tmp)]
     out = _run(cmd)
     os.replace(tmp, target)

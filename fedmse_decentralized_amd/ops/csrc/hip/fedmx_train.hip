@@ -44,6 +44,9 @@
 // patterns; 4: iglp_opt(0) (fastest measured with the compact order and the
 // FMA-form Adam: 1.211 vs 1.231 ms compiler / 1.257 ms pattern 1 per
 // 5-client x 5-epoch launch); 5: iglp_opt(1)
+#ifndef FEDMX_DW4_LATE
+#define FEDMX_DW4_LATE 0
+#endif
 #ifndef FEDMX_SCHED_HINTS
 #define FEDMX_SCHED_HINTS 4
 #endif
@@ -131,6 +134,35 @@ __device__ __forceinline__ void lds_to_slab(Slab& o, const Lane& L) {
       for (int v = 0; v < 2; ++v) o.q4[v][t][r] = L.w4[(16 * v + r) * S_W4 + 16 * t];
 #pragma unroll
   for (int r = 0; r < 4; ++r) o.o[r] = L.own[r * L.own_stride];
+}
+
+// 16x16 product summed over the two 16-wide halves of the hidden axis
+// (k-steps (t, s)): L2 (W2a H1) and dZ (W3a^T dH3).  These are the dependent
+// chains on the step's critical path (one accumulator: 7-8 x 40-cycle MFMA
+// latency); FEDMX_SPLIT_CHAINS sums each half in its own accumulator and adds
+// the two, so the chain is ~half as long.
+#ifndef FEDMX_SPLIT_CHAINS
+#define FEDMX_SPLIT_CHAINS 0
+#endif
+template <bool CP>
+__device__ __forceinline__ f32x4 chain2(f32x4 a0, f32x4 a1, f32x4 b0, f32x4 b1) {
+  f32x4 x = zero4();
+#if FEDMX_SPLIT_CHAINS
+  f32x4 y = zero4();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    x = mfma16(a0[s], b0[s], x);
+    if (s < (CP ? 3 : 4)) y = mfma16(a1[s], b1[s], y);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) x[r] = x[r] + y[r];
+#else
+#pragma unroll
+  for (int s = 0; s < 4; ++s) x = mfma16(a0[s], b0[s], x);
+#pragma unroll
+  for (int s = 0; s < (CP ? 3 : 4); ++s) x = mfma16(a1[s], b1[s], x);
+#endif
+  return x;
 }
 
 // One batch column tile ("chunk") of up to 16 rows, in the two register
@@ -364,15 +396,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       h1[t] = s;
     }
     parity ^= 1;
-    z = zero4();
-    {
-      const f32x4 a0 = lds_read4(a2p);
-      const f32x4 a1 = lds_read4(a2p + 16);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) z = mfma16(a0[s], h1[0][s], z);
-#pragma unroll
-      for (int s = 0; s < (CP ? 3 : 4); ++s) z = mfma16(a1[s], h1[1][s], z);
-    }
+    z = chain2<CP>(lds_read4(a2p), lds_read4(a2p + 16), h1[0], h1[1]);
     zb = z;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -494,15 +518,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       h1[0] = sum0;
       h1[1] = sum1;
     }
-    f32x4 z = zero4();
-    {
-      const f32x4 a0 = lds_read4(a2p);
-      const f32x4 a1 = lds_read4(a2p + 16);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) z = mfma16(a0[s], h1[0][s], z);
-#pragma unroll
-      for (int s = 0; s < (CP ? 3 : 4); ++s) z = mfma16(a1[s], h1[1][s], z);
-    }
+    const f32x4 z = chain2<CP>(lds_read4(a2p), lds_read4(a2p + 16), h1[0], h1[1]);
     f32x4 zb = z;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -610,6 +626,13 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       const int bc_n = has_next ? min(16, min(B, n_tr - bi_n * B) - 16 * ch_n) : 0;
       const float inv_bt = 1.0f / (float)bt;
       if (ch == 0) {
+        // bias corrections of the Adam step this batch closes (python:
+        // 1 - beta ** step), computed at the batch start, off the critical path
+        b1pow *= (double)A.beta1;
+        b2pow *= (double)A.beta2;
+        K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
+        K.bc2s = (float)sqrt(1.0 - b2pow);
+        K.inv_bc2s = 1.0f / K.bc2s;
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -674,24 +697,29 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       }
       STAMP(stamp_on, 4);
       wave_sync();
-      // ---- dW4 (own rows) accumulated over the batch's chunks
-      {
-        const f32x4 a0 = lds_read4(sT0 + tr);
-        const f32x4 a1 = lds_read4(sT0 + tr + 16 * S_T);
-        const f32x4 b0 = lds_read4(sT1 + tr);
-        const f32x4 b1 = lds_read4(sT1 + tr + 16 * S_T);
+      // ---- dW4 (own rows) accumulated over the batch's chunks.  Operands are
+      // read here (sT0 is reused for dH3^T below); with FEDMX_DW4_LATE the
+      // products are issued after barrier #2, off the path to the barrier,
+      // where they fill the MFMA gaps of the dependent dZ / dH1 chains.
+      const f32x4 w4a0 = lds_read4(sT0 + tr);
+      const f32x4 w4a1 = lds_read4(sT0 + tr + 16 * S_T);
+      const f32x4 w4b0 = lds_read4(sT1 + tr);
+      const f32x4 w4b1 = lds_read4(sT1 + tr + 16 * S_T);
+      auto dw4_products = [&]() {
 #pragma unroll
         for (int s = 0; s < KB; ++s) {
-          G4[0][0] = mfma16(a0[s], b0[s], G4[0][0]);
-          G4[0][1] = mfma16(a0[s], b1[s], G4[0][1]);
-          G4[1][0] = mfma16(a1[s], b0[s], G4[1][0]);
-          G4[1][1] = mfma16(a1[s], b1[s], G4[1][1]);
+          G4[0][0] = mfma16(w4a0[s], w4b0[s], G4[0][0]);
+          G4[0][1] = mfma16(w4a0[s], w4b1[s], G4[0][1]);
+          G4[1][0] = mfma16(w4a1[s], w4b0[s], G4[1][0]);
+          G4[1][1] = mfma16(w4a1[s], w4b1[s], G4[1][1]);
         }
-      }
+      };
+      if (!FEDMX_DW4_LATE) dw4_products();
       STAMP(stamp_on, 5);
       STAMP(stamp_on, 6);
       __syncthreads();  // barrier #2: dH3 partials of all waves visible
       STAMP(stamp_on, 7);
+      if (FEDMX_DW4_LATE) dw4_products();
       f32x4 dh3[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -711,11 +739,6 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       float prox_acc = 0.f;  // sum (p - anchor)^2 of owned params (pre-update)
       if (last) {
         ++step;
-        b1pow *= (double)A.beta1;
-        b2pow *= (double)A.beta2;
-        K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
-        K.bc2s = (float)sqrt(1.0 - b2pow);
-        K.inv_bc2s = 1.0f / K.bc2s;
         // W4 is not read again this step (its dH3 product ran before barrier
         // #2): update it here, where its VALU work overlaps the backward MFMAs
 #pragma unroll
@@ -735,11 +758,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         for (int r = 0; r < 4; ++r) sT0[tw + (16 * t + r) * S_T] = dh3[t][r];
       // ---- dZ = W3a^T dH3 (pre-update W3, every wave), + shrink-loss gradient
       //      lambda/B * z / ||z|| (0 where ||z|| == 0)
-      f32x4 dz = zero4();
-#pragma unroll
-      for (int s = 0; s < 4; ++s) dz = mfma16(q3[0][s], dh3[0][s], dz);
-#pragma unroll
-      for (int s = 0; s < (CP ? 3 : 4); ++s) dz = mfma16(q3[1][s], dh3[1][s], dz);
+      f32x4 dz = chain2<CP>(f32x4{q3[0][0], q3[0][1], q3[0][2], q3[0][3]},
+                            f32x4{q3[1][0], q3[1][1], q3[1][2], q3[1][3]}, dh3[0], dh3[1]);
       const float shr_raw = lam * __builtin_amdgcn_rcpf((float)bt * norm_c);
       const float shr = (col_ok && norm_c > 0.f) ? shr_raw : 0.f;
 #pragma unroll

@@ -19,6 +19,9 @@ from fedmse_decentralized_amd.ops import build  # noqa: E402
 VARIANTS = {
     "base": [],                                   # defaults: FMA-form Adam, iglp_opt(0)
     "sched0": ["-DFEDMX_SCHED_HINTS=0"],          # compiler schedule
+    "dw4late": ["-DFEDMX_DW4_LATE=1"],            # dW4 products after barrier #2
+    "split": ["-DFEDMX_SPLIT_CHAINS=1"],          # L2 / dZ as two accumulator chains
+    "novgprform": ["-mllvm", "-amdgpu-mfma-vgpr-form=0"],  # compiler's AGPR/VGPR choice
     "noslp": ["-fno-slp-vectorize"],
     "sepadam": ["-DFEDMX_ADAM_FMA=0"],
     "hint1": ["-DFEDMX_SCHED_HINTS=1"],           # 64 x (1 MFMA, 6 VALU)
