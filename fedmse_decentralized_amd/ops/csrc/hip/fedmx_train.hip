@@ -269,13 +269,6 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   const int xcol = 32 * w + 4 * g;
   const float lam = A.lambda;
   const float inv_d = 1.0f / (float)d_in;
-  // loop-invariant feature masks as 0/1 multipliers (own 8 feature rows)
-  float fm0[4], fm1[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    fm0[r] = (xcol + r < d_in) ? 1.f : 0.f;
-    fm1[r] = (xcol + 16 + r < d_in) ? 1.f : 0.f;
-  }
   // hidden / latent positions of this lane's D-layout registers (16t + 4g + r,
   // 4g + r) and of its batch-major column (16t + c): real / bias flags
   bool hreal_d[2][4], hbias_d[2][4], zreal_d[4], zbias_d[4], hreal_c[2];
@@ -303,44 +296,34 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   bool stamp_fwd = false;
   (void)stamp_fwd;
 
-  // rows [row0, row0 + bc) of X, bc in 1..16.  Branch-free prefetch: rows
-  // past the chunk read row0 (always valid); the zeroing / bias column are
-  // applied by finalize_chunk when the chunk is consumed, so issuing the
-  // loads never waits for them.
+  // rows [row0, row0 + bc) of X, bc in 1..16.  Branch-free prefetch: tile
+  // columns / rows past the chunk read row0 (always valid) and keep that
+  // duplicated data: every product that sums over the batch meets them with an
+  // exactly zero gradient (dY is scaled by 0 there, so dH3, dZ and dH1 are 0
+  // too) and the loss masks them, so they never need zeroing.  The bias input
+  // (feature DP-1) is set by finalize_chunk when the chunk is consumed, so
+  // issuing the loads never waits.
   auto load_chunk = [&](const float* X, int row0, int bc, XChunk& x) {
     const float* src = X + (size_t)(row0 + ((unsigned)brow_c < (unsigned)bc ? brow_c : 0)) * DP + xcol;
     x.f0 = *reinterpret_cast<const f32x4*>(src);
     x.f1 = *reinterpret_cast<const f32x4*>(src + 16);
     const float* bsrc = X + (size_t)row0 * DP + 32 * w + c;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < (CP ? 3 : 4); ++r) {   // CP: row quad 3 is padding, never read
       const int rr = ((unsigned)brow_b[r] < (unsigned)bc) ? brow_b[r] : 0;
       x.b0[r] = bsrc[(size_t)rr * DP];
       x.b1[r] = bsrc[(size_t)rr * DP + 16];
     }
+    if (CP) {
+      x.b0[3] = 0.f;
+      x.b1[3] = 0.f;
+    }
   };
   auto finalize_chunk = [&](int bc, XChunk& x) {
-    const bool ok = (unsigned)brow_c < (unsigned)bc;
+    (void)bc;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool okr = (unsigned)brow_b[r] < (unsigned)bc;
-      x.f0[r] = ok ? x.f0[r] : 0.f;
-      x.f1[r] = ok ? x.f1[r] : 0.f;
-      x.b0[r] = okr ? x.b0[r] : 0.f;
-      x.b1[r] = okr ? (bias_col ? 1.f : x.b1[r]) : 0.f;
-    }
-    if (bias_lane) x.f1[3] = 1.f;
-  };
-  auto load_chunk_f = [&](const float* X, int row0, int bc, XChunk& x) {  // validation: feature-major only
-    const bool ok = (unsigned)brow_c < (unsigned)bc;
-    const float* src = X + (size_t)(row0 + (ok ? brow_c : 0)) * DP + xcol;
-    const f32x4 f0 = *reinterpret_cast<const f32x4*>(src);
-    const f32x4 f1 = *reinterpret_cast<const f32x4*>(src + 16);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      x.f0[r] = ok ? f0[r] : 0.f;
-      x.f1[r] = ok ? f1[r] : 0.f;
-    }
+    for (int r = 0; r < (CP ? 3 : 4); ++r)
+      if (bias_col) x.b1[r] = 1.f;
     if (bias_lane) x.f1[3] = 1.f;
   };
 
@@ -443,8 +426,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
     float sq = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float d0 = (y[0][r] - x.f0[r]) * fm0[r];
-      const float d1 = (y[1][r] - x.f1[r]) * fm1[r];
+      // padded features: Y = 0 (zero W4 rows) and X = 0; only the bias
+      // input (feature DP-1, X = 1) is masked
+      const float d0 = y[0][r] - x.f0[r];
+      const float d1 = (bias_lane && r == 3) ? 0.f : y[1][r] - x.f1[r];
       sq += d0 * d0 + d1 * d1;
     }
     const bool col_ok = (unsigned)brow_c < (unsigned)bc;
@@ -475,7 +460,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       for (int v = 0; v < 2; ++v) {
         const f32x4 q = *reinterpret_cast<const f32x4*>(src + 32 * b + 16 * v);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xf[b][v][r] = ok ? q[r] : 0.f;
+        for (int r = 0; r < 4; ++r) xf[b][v][r] = q[r];
       }
     if (g == 3) xf[3][1][3] = 1.f;   // bias column DP-1
     f32x4 h1[2];
@@ -570,10 +555,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       float sq = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float m0 = (32 * b + 4 * g + r < d_in) ? 1.f : 0.f;
-        const float m1 = (32 * b + 16 + 4 * g + r < d_in) ? 1.f : 0.f;
-        const float d0 = (acc0[r] - xf[b][0][r]) * m0;
-        const float d1 = (acc1[r] - xf[b][1][r]) * m1;
+        const float d0 = acc0[r] - xf[b][0][r];
+        const float d1 = (b == 3 && g == 3 && r == 3) ? 0.f : acc1[r] - xf[b][1][r];
         sq += d0 * d0 + d1 * d1;
       }
       sq = ok ? sq : 0.f;
@@ -668,8 +651,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       f32x4 dy[2];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        dy[0][r] = (y[0][r] - cur.f0[r]) * (scale * fm0[r]);
-        dy[1][r] = (y[1][r] - cur.f1[r]) * (scale * fm1[r]);
+        dy[0][r] = (y[0][r] - cur.f0[r]) * scale;
+        dy[1][r] = (bias_lane && r == 3) ? 0.f : (y[1][r] - cur.f1[r]) * scale;
         sT0[tw + r * S_T] = dy[0][r];
         sT0[tw + (16 + r) * S_T] = dy[1][r];
         sT1[tw + r * S_T] = h3[0][r];
