@@ -228,22 +228,28 @@ class DeviceRound:
                 per_rank: Dict[int, List[int]] = {}
                 for c in selected:
                     per_rank.setdefault(fed.shard.owner(c), []).append(c)
+                # Packing / unpacking index arrays go through the mapped
+                # descriptor ring into row-copy kernels: no host -> device
+                # copies, which (from pageable memory) would synchronise the
+                # host with the training kernel every round.  Rows past a
+                # rank's selection are never read, so `send` needs no fill.
                 slots = max(len(v) for v in per_rank.values())
                 mine = per_rank.get(comm.rank, [])
-                send = torch.zeros(slots + 1, P_PAD, dtype=torch.float32, device=dev)
+                send = torch.empty(slots + 1, P_PAD, dtype=torch.float32, device=dev)
                 if mine:
-                    idx = torch.tensor([self._loc(c) for c in mine], dtype=torch.long, device=dev)
-                    send[:len(mine)] = st.params.index_select(0, idx)
-                    cid = torch.tensor(mine, dtype=torch.long, device=dev)
-                    send[slots].view(torch.float64)[:4 * len(mine)].view(-1, 4).copy_(self.vec.index_select(0, cid))
+                    loc_ptr, cid_ptr = self.rt.desc.put(np.asarray([self._loc(c) for c in mine], dtype=np.int32),
+                                                        np.asarray(mine, dtype=np.int32))
+                    _hip.copy_rows(send.data_ptr(), P_PAD, 0, st.params.data_ptr(), P_PAD, loc_ptr, len(mine),
+                                   P_PAD, dev)
+                    # vote records: 4 doubles = 8 floats per client, packed into the tail row
+                    _hip.copy_rows(send[slots].data_ptr(), 8, 0, self.vec.data_ptr(), 8, cid_ptr, len(mine), 8, dev)
                 allg = comm.all_gather(send).reshape(-1, P_PAD)          # [world * (slots+1), P]
-                tails = allg.view(comm.world_size, slots + 1, P_PAD)[:, slots]
-                recs = tails.contiguous().view(torch.float64)[:, :4 * slots].reshape(comm.world_size * slots, 4)
                 owners = [fed.shard.owner(c) for c in selected]
-                src = torch.tensor([o * slots + per_rank[o].index(c) for o, c in zip(owners, selected)],
-                                   dtype=torch.long, device=dev)
-                dst = torch.tensor(list(selected), dtype=torch.long, device=dev)
-                self.vec.index_copy_(0, dst, recs.index_select(0, src))
+                # record of client c: tail row of its owner, entry j (8-float units)
+                src = np.asarray([((o * (slots + 1) + slots) * P_PAD) // 8 + per_rank[o].index(c)
+                                  for o, c in zip(owners, selected)], dtype=np.int32)
+                src_ptr, dst_ptr = self.rt.desc.put(src, np.asarray(selected, dtype=np.int32))
+                _hip.copy_rows(self.vec.data_ptr(), 8, dst_ptr, allg.data_ptr(), 8, src_ptr, k, 8, dev)
                 base = allg
                 rows = np.asarray([o * (slots + 1) + per_rank[o].index(c) for o, c in zip(owners, selected)],
                                   dtype=np.int64)

@@ -121,6 +121,7 @@ def lib():
                 "fedmx_decide_adopt": [ctypes.POINTER(DecideArgs), vp],
                 "fedmx_copy_f64": [vp, vp, i32, vp],
                 "fedmx_copy2_f64": [vp, vp, i32, vp, vp, i32, vp],
+                "fedmx_copy_rows": [vp, i32, vp, vp, i32, vp, i32, i32, vp],
                 "fedmx_protocol_sizes": [vp],
             }
             for name, args in sig.items():
@@ -406,6 +407,14 @@ def copy_f64(dst_ptr: int, src_ptr: int, n: int, device):
 
 def copy2_f64(d0: int, s0: int, n0: int, d1: int, s1: int, n1: int, device):
     _check(lib().fedmx_copy2_f64(d0, s0, n0, d1, s1, n1, _stream(device)), "fedmx_copy2_f64")
+
+
+def copy_rows(dst_ptr: int, dstride: int, didx_ptr: int, src_ptr: int, sstride: int, sidx_ptr: int, n: int,
+              length: int, device):
+    """dst[didx[i]] = src[sidx[i]] for n rows of ``length`` floats (index
+    pointers may be 0 = identity; strides in floats)."""
+    _check(lib().fedmx_copy_rows(dst_ptr, dstride, didx_ptr, src_ptr, sstride, sidx_ptr, n, length,
+                                 _stream(device)), "fedmx_copy_rows")
 
 
 def broadcast_rows(dst0: torch.Tensor, dst1: Optional[torch.Tensor], rows: Sequence[int], src: torch.Tensor):

@@ -246,9 +246,34 @@ __global__ __launch_bounds__(256) void copy2_f64_kernel(double* __restrict__ d0,
   }
 }
 
+// Row gather / scatter: dst[(didx ? didx[i] : i) * dstride + j] =
+// src[(sidx ? sidx[i] : i) * sstride + j] for i < n, j < len (floats; len and
+// the strides are multiples of 4).  Index arrays usually live in the mapped
+// descriptor ring, so packing the multi-rank exchange needs no host copies.
+__global__ __launch_bounds__(256) void copy_rows_kernel(float* __restrict__ dst, int dstride,
+                                                        const int32_t* __restrict__ didx,
+                                                        const float* __restrict__ src, int sstride,
+                                                        const int32_t* __restrict__ sidx, int len) {
+  const int i = blockIdx.y;
+  const int j = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (j >= len) return;
+  const size_t d = (size_t)(didx ? didx[i] : i) * dstride + j;
+  const size_t s = (size_t)(sidx ? sidx[i] : i) * sstride + j;
+  *reinterpret_cast<f32x4*>(dst + d) = *reinterpret_cast<const f32x4*>(src + s);
+}
+
 }  // namespace fedmx
 
 extern "C" {
+
+int fedmx_copy_rows(float* dst, int dstride, const int32_t* didx, const float* src, int sstride, const int32_t* sidx,
+                    int n, int len, hipStream_t stream) {
+  if (n <= 0 || len <= 0) return 0;
+  if (len % 4 || dstride % 4 || sstride % 4 || n > 65535) return -1;
+  hipLaunchKernelGGL(fedmx::copy_rows_kernel, dim3((len / 4 + 255) / 256, n), dim3(256), 0, stream, dst, dstride,
+                     didx, src, sstride, sidx, len);
+  return (int)hipGetLastError();
+}
 
 int fedmx_copy2_f64(double* d0, const double* s0, int n0, double* d1, const double* s1, int n1, hipStream_t stream) {
   const int n = max(n0, n1);
