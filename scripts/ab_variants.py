@@ -17,17 +17,14 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from fedmse_decentralized_amd.ops import build  # noqa: E402
 
 VARIANTS = {
-    "base": [],                                   # defaults: FMA-form Adam, iglp_opt(0)
-    "sched0": ["-DFEDMX_SCHED_HINTS=0"],          # compiler schedule
-    "dw4late": ["-DFEDMX_DW4_LATE=1"],            # dW4 products after barrier #2
-    "split": ["-DFEDMX_SPLIT_CHAINS=1"],          # L2 / dZ as two accumulator chains
-    "novgprform": ["-mllvm", "-amdgpu-mfma-vgpr-form=0"],  # compiler's AGPR/VGPR choice
-    "noslp": ["-fno-slp-vectorize"],
-    "sepadam": ["-DFEDMX_ADAM_FMA=0"],
-    "hint1": ["-DFEDMX_SCHED_HINTS=1"],           # 64 x (1 MFMA, 6 VALU)
-    "hint2": ["-DFEDMX_SCHED_HINTS=2"],           # 48 x (1 MFMA, 4 VALU)
-    "hint3": ["-DFEDMX_SCHED_HINTS=3"],           # 48 x (1 MFMA, 10 VALU)
-    "iglp1": ["-DFEDMX_SCHED_HINTS=5"],
+    "base": [],                                   # defaults: compact order, FMA Adam, iglp_opt(0), VGPR-form MFMA
+    "sched0": ["-DFEDMX_SCHED_HINTS=0"],          # compiler schedule          (+2.5%, measured)
+    "hint1": ["-DFEDMX_SCHED_HINTS=1"],           # 64 x (1 MFMA, 6 VALU)      (+9%)
+    "sepadam": ["-DFEDMX_ADAM_FMA=0"],            # separately rounded Adam    (+3%)
+    "dw4late": ["-DFEDMX_DW4_LATE=1"],            # dW4 products after barrier #2 (+0.5%)
+    "split": ["-DFEDMX_SPLIT_CHAINS=1"],          # L2 / dZ as two accumulator chains (+0.3%)
+    "novgprform": ["-mllvm", "-amdgpu-mfma-vgpr-form=0"],  # AGPR accumulators (+3.3%)
+    "noslp": ["-fno-slp-vectorize"],              # no packed fp32 VALU        (+5%)
 }
 
 
