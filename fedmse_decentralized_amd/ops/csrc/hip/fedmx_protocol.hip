@@ -56,7 +56,81 @@ static_assert(sizeof(WsumArgs) == 48, "WsumArgs layout is shared with Python");
 __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, const WsumArgs W) {
   __shared__ float s_w[1024];
   __shared__ int s_agg;
-  if (threadIdx.x == 0) {
+  const int tid = threadIdx.x;
+  if (E.k <= 64) {
+    // Small selections (every reference config): wave 0 stages the inputs
+    // with one parallel load each (the noise table lives in mapped host
+    // memory: one PCIe round trip instead of one per draw); each candidate
+    // lane forms its noisy score, then the reference's serial first-minimum
+    // scan runs over the lanes.  Same double arithmetic as the serial loop
+    // below (bit-identical decisions).
+    __shared__ double s_noise[64 * 63];
+    __shared__ double s_inv[64];
+    if (tid < 64) {
+      const int lane = tid;
+      const int k = E.k;
+      int c = -1, cnt = 0;
+      double vs = 0.0, mse = 1.0;
+      if (lane < k) {
+        c = E.sel[lane];
+        vs = E.vec[(size_t)c * 4];
+        mse = E.vec[(size_t)c * 4 + 3];
+        cnt = E.agg_counts[c];
+      }
+      for (int i = lane; i < k * (k - 1); i += 64) s_noise[i] = E.noise[i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      int agg = -1, voter = -1;
+      for (int vi = 0; vi < k && agg < 0; ++vi) {
+        const int v = __shfl(c, vi, 64);
+        // candidate lane ci != vi draws noise entry j = ci - (ci > vi)
+        bool cand = lane < k && lane != vi && cnt < E.cap;
+        double sc = 0.0;
+        if (lane < k && lane != vi) {
+          const double f = 1.0 + (s_noise[(size_t)vi * (k - 1) + lane - (lane > vi ? 1 : 0)] - 0.5) * 0.0002;
+          sc = vs * f;
+        }
+        // the serial scan of the reference loop over the candidates' lanes
+        // (uniform across the wave; NaN scores behave exactly as there)
+        int best = -1;
+        double best_s = 0.0;
+        for (int ci = 0; ci < k; ++ci) {
+          const double s_ci = __shfl(sc, ci, 64);
+          const int ok_ci = __shfl(cand ? 1 : 0, ci, 64);
+          if (ok_ci && (best < 0 || s_ci < best_s)) {
+            best = ci;
+            best_s = s_ci;
+          }
+        }
+        if (best >= 0) {
+          agg = __shfl(c, best, 64);
+          voter = v;
+        }
+      }
+      if (lane == 0) s_agg = agg;
+      if (agg >= 0) {
+        if (E.rule == 1) {
+          if (lane < k) s_inv[lane] = 1.0 / mse;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          double tot = 0.0;
+          for (int j = 0; j < k; ++j) tot += s_inv[j];   // selection order, as the serial form
+          if (lane < k) s_w[lane] = (float)(s_inv[lane] / tot);
+        } else if (lane < k) {
+          s_w[lane] = (float)(1.0 / (double)k);
+        }
+      }
+      if (blockIdx.x == 0 && lane == 0) {
+        E.state[0] = agg;
+        E.state[1] = voter;
+        E.report[0] = agg;
+        E.report[1] = voter;
+      }
+      if (blockIdx.x == 0 && agg >= 0 && lane < k) E.weights[lane] = s_w[lane];
+    }
+  } else if (tid == 0) {
     int agg = -1, voter = -1;
     for (int vi = 0; vi < E.k && agg < 0; ++vi) {
       const int v = E.sel[vi];
@@ -162,8 +236,10 @@ __global__ __launch_bounds__(1024) void decide_adopt_kernel(const DecideArgs A) 
     const float* sp = A.sse + A.sse_off[cl];
     const int n = A.sse_n[cl];
     double sv = 0.0;
-    if (tid < 256)
+    if (tid < 256) {
+#pragma unroll 8
       for (int r = tid; r < n; r += 256) sv += (double)sp[r];
+    }
     for (int o = 32; o >= 1; o >>= 1) sv += __shfl_xor(sv, o, 64);
     if (lane == 0 && wv < 4) s_d[wv] = sv;
     __syncthreads();
