@@ -110,6 +110,7 @@ def main(argv=None):
         prof = cProfile.Profile()
         prof.enable()
     t0 = time.perf_counter()
+    w_busy0 = fed.writer.busy_s
     last = None
     for _ in range(args.steps):
         last = one_round()
@@ -168,6 +169,7 @@ def main(argv=None):
             "detection_auc_mean": round(auc, 6),
             "detection_auc_min": round(float(np.min(last.metrics)), 6) if last is not None else None,
             "phase_ms_total": {k: round(v, 3) for k, v in fed.tel.summary().items()},
+            "writer_busy_ms_per_round": round(1e3 * (fed.writer.busy_s - w_busy0) / args.steps, 4),
         }
         line = json.dumps(rec)
         print(line, flush=True)

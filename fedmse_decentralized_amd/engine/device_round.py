@@ -303,7 +303,8 @@ class DeviceRound:
             if local_sel and cfg.save_checkpoints:
                 si = self.snap_i
                 self.snap_i = (si + 1) % self.n_snap
-                self.snap_free[si].wait()
+                with tel.phase("wait_writer"):   # artefact writer backlog (host-bound indicator)
+                    self.snap_free[si].wait()
                 self.snap_free[si].clear()
                 nd = st.best.numel() // 2
                 _hip.copy2_f64(self.snap_buf.dev_ptr + si * st.best.numel() * 4, self.best_stage.data_ptr(), nd,
@@ -332,7 +333,8 @@ class DeviceRound:
         res = LazyRoundResult(self, rec)
         # bounded run-ahead: collect rounds that are max_pending behind (normally already finished)
         while len(self.pending) > self.max_pending:
-            self._collect(self.pending.popleft())
+            with tel.phase("collect"):    # mostly waiting for round r-2 on the GPU
+                self._collect(self.pending.popleft())
         if cfg.global_early_stop:
             self.collect_until(rnd)
         return res

@@ -235,10 +235,11 @@ class Federation:
 
     # -- report / artefact submission (background writer) ---------------------------
     def _report_round(self, rnd: int, metrics: np.ndarray) -> None:
-        reports.append_round_result(self.cfg, self.run, rnd, metrics, self.model_type, self.update_type)
+        reports.append_round_result(self.cfg, self.run, rnd, metrics, self.model_type, self.update_type,
+                                    files=self.writer.files)
 
     def _report_verification(self, rnd: int, vr: List[Dict]) -> None:
-        reports.append_verification(self.cfg, self.run, rnd, vr)
+        reports.append_verification(self.cfg, self.run, rnd, vr, files=self.writer.files)
 
     def _submit_checkpoints(self, res, local_sel: Sequence[int], snap, ev) -> None:
         dims = self.dims
@@ -249,10 +250,10 @@ class Federation:
             improved = res.best_epoch[i] >= 0
             trk = list(res.tracking[i])
 
-            def job(d=d, row=row, improved=improved, trk=trk):
+            def job(d=d, row=row, improved=improved, trk=trk, files=self.writer.files):
                 if improved:
-                    ckpt.save_model_cpt_fast(d, snap[row].numpy()[cidx], dims)
-                ckpt.save_tracking(d, trk)
+                    ckpt.save_model_cpt_fast(d, snap[row].numpy()[cidx], dims, files=files)
+                ckpt.save_tracking(d, trk, files=files)
             self.writer.submit(job, ev)
 
     def _resume_path(self, base: str) -> str:

@@ -13,10 +13,13 @@ from __future__ import annotations
 
 import queue
 import threading
+import time
 import traceback
 from typing import Callable, Optional
 
 import torch
+
+from .files import ArtifactFiles
 
 
 class AsyncWriter:
@@ -24,6 +27,9 @@ class AsyncWriter:
         self.enabled = enabled
         self.q: "queue.Queue" = queue.Queue()
         self.errors = []
+        self.files = ArtifactFiles()   # used only from the job context (writer thread)
+        self.busy_s = 0.0   # time spent running jobs (telemetry)
+        self.jobs = 0
         self.t: Optional[threading.Thread] = None
         if enabled:
             self.t = threading.Thread(target=self._run, name="fedmx-writer", daemon=True)
@@ -39,7 +45,10 @@ class AsyncWriter:
             try:
                 if event is not None:
                     event.synchronize()
+                t0 = time.perf_counter()
                 fn()
+                self.busy_s += time.perf_counter() - t0
+                self.jobs += 1
             except Exception:  # pragma: no cover - surfaced by flush()
                 self.errors.append(traceback.format_exc())
             finally:
@@ -56,6 +65,9 @@ class AsyncWriter:
     def flush(self):
         if self.enabled:
             self.q.join()
+        # the queue is drained (no job running): release the cached
+        # descriptors, so files deleted or replaced between sweeps are reopened
+        self.files.close()
         if self.errors:
             errs, self.errors = self.errors, []
             raise RuntimeError("artefact writer failed:\n" + "\n".join(errs))
@@ -66,6 +78,7 @@ class AsyncWriter:
             self.q.put(None)
             self.t.join()
             self.t = None
+        self.files.close()
 
 
 def snapshot_to_host(t: torch.Tensor):

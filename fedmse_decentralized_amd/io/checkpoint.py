@@ -94,13 +94,18 @@ def _state_metadata():
     return meta
 
 
-def save_model_cpt_fast(save_dir: str, canonical: np.ndarray, dims: ModelDims = DEFAULT_DIMS) -> str:
-    """``model.cpt`` from a canonical parameter vector via the byte template."""
+def save_model_cpt_fast(save_dir: str, canonical: np.ndarray, dims: ModelDims = DEFAULT_DIMS,
+                        files=None) -> str:
+    """``model.cpt`` from a canonical parameter vector via the byte template
+    (``files``: an ``io.files.ArtifactFiles`` cache — rewrite in place)."""
     tpl = _TEMPLATES.get(dims)
     if tpl is None:
         tpl = _TEMPLATES[dims] = _CptTemplate(dims)
-    os.makedirs(save_dir, exist_ok=True)
     path = os.path.join(save_dir, "model.cpt")
+    if files is not None:
+        files.overwrite(path, tpl.render(canonical))
+        return path
+    os.makedirs(save_dir, exist_ok=True)
     with open(path, "wb") as f:
         f.write(tpl.render(canonical))
     return path
@@ -126,11 +131,15 @@ def save_model_cpt(save_dir: str, padded_params: torch.Tensor, dims: ModelDims =
     return path
 
 
-def save_tracking(save_dir: str, tracking: Sequence[Tuple[float, float]]) -> str:
-    os.makedirs(save_dir, exist_ok=True)
+def save_tracking(save_dir: str, tracking: Sequence[Tuple[float, float]], files=None) -> str:
     path = os.path.join(save_dir, "training_tracking.pkl")
+    blob = pickle.dumps([(float(a), float(b)) for a, b in tracking], protocol=4)
+    if files is not None:
+        files.overwrite(path, blob)
+        return path
+    os.makedirs(save_dir, exist_ok=True)
     with open(path, "wb") as f:
-        pickle.dump([(float(a), float(b)) for a, b in tracking], f, protocol=4)
+        f.write(blob)
     return path
 
 

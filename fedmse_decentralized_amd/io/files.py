@@ -1,0 +1,76 @@
+"""Open-file cache for the per-round artefacts.
+
+Every round rewrites each trained client's ``model.cpt`` and
+``training_tracking.pkl`` and appends one line to each JSONL report.  On the
+overlay / ext4 filesystems of the GPU hosts, ``open(path, "wb")`` — a
+truncate followed by re-allocating the blocks — costs ~130 us per file, which
+made the background writer the slowest stage of a ~1.1 ms round.  Here files
+stay open: a rewrite is one ``pwrite`` at offset 0 (plus ``ftruncate`` only
+when the content got shorter — ``model.cpt`` has a fixed size for fixed
+model dims), an append one ``write`` on an ``O_APPEND`` descriptor (~3 us
+each).  The bytes on disk are exactly what ``open(..., "wb"/"a")`` would
+leave.  Not thread-safe: owned by the single writer thread.
+"""
+from __future__ import annotations
+
+import os
+from collections import OrderedDict
+from typing import Dict, Tuple
+
+
+class ArtifactFiles:
+    def __init__(self, max_open: int = 512):
+        self.max_open = max_open
+        self._fds: "OrderedDict[Tuple[str, str], int]" = OrderedDict()
+        self._size: Dict[str, int] = {}
+
+    def _fd(self, path: str, mode: str) -> int:
+        key = (path, mode)
+        fd = self._fds.get(key)
+        if fd is not None:
+            self._fds.move_to_end(key)
+            return fd
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        if mode == "w":
+            fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
+            self._size[path] = os.fstat(fd).st_size
+        else:
+            fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644)
+        self._fds[key] = fd
+        while len(self._fds) > self.max_open:
+            (p, m), old = self._fds.popitem(last=False)
+            os.close(old)
+        return fd
+
+    def overwrite(self, path: str, data: bytes) -> None:
+        """File content becomes exactly ``data``."""
+        fd = self._fd(path, "w")
+        n = len(data)
+        view = memoryview(data)
+        off = 0
+        while off < n:
+            off += os.pwrite(fd, view[off:], off)
+        if self._size.get(path, 0) > n:
+            os.ftruncate(fd, n)
+        self._size[path] = n
+
+    def append(self, path: str, data: bytes) -> None:
+        fd = self._fd(path, "a")
+        view = memoryview(data)
+        off = 0
+        while off < len(data):
+            off += os.write(fd, view[off:])
+
+    def close(self) -> None:
+        for fd in self._fds.values():
+            os.close(fd)
+        self._fds.clear()
+        self._size.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

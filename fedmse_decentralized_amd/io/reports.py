@@ -22,18 +22,26 @@ def results_path(cfg, run: int, model_type: str, update_type: str) -> str:
     return os.path.join(directory, f"{cfg.scen_name}_{cfg.num_participants}_{model_type}_{update_type}_results.json")
 
 
-def append_round_result(cfg, run: int, rnd: int, metrics: Sequence[float], model_type: str, update_type: str) -> str:
-    path = results_path(cfg, run, model_type, update_type)
+def _append_line(path: str, obj, files=None) -> None:
+    line = json.dumps(obj) + "\n"   # json.dump(obj, f); f.write("\n") writes these bytes
+    if files is not None:
+        files.append(path, line.encode())
+        return
     os.makedirs(os.path.dirname(path), exist_ok=True)
     with open(path, "a") as f:
-        json.dump({
-            "round": rnd + 1,
-            "client_metrics": [float(s) for s in metrics],
-            "update_type": update_type,
-            "model_type": model_type,
-            "global_loss": min(metrics) if len(metrics) else float("inf"),
-        }, f)
-        f.write("\n")
+        f.write(line)
+
+
+def append_round_result(cfg, run: int, rnd: int, metrics: Sequence[float], model_type: str, update_type: str,
+                        files=None) -> str:
+    path = results_path(cfg, run, model_type, update_type)
+    _append_line(path, {
+        "round": rnd + 1,
+        "client_metrics": [float(s) for s in metrics],
+        "update_type": update_type,
+        "model_type": model_type,
+        "global_loss": min(metrics) if len(metrics) else float("inf"),
+    }, files)
     return path
 
 
@@ -41,12 +49,9 @@ def verification_path(cfg, run: int) -> str:
     return os.path.join(cfg.checkpoint_dir, f"Run_{run}", "verification_results.json")
 
 
-def append_verification(cfg, run: int, rnd: int, results: List[Dict]) -> str:
+def append_verification(cfg, run: int, rnd: int, results: List[Dict], files=None) -> str:
     path = verification_path(cfg, run)
-    os.makedirs(os.path.dirname(path), exist_ok=True)
-    with open(path, "a") as f:
-        json.dump({"round": rnd + 1, "verification_results": results}, f)
-        f.write("\n")
+    _append_line(path, {"round": rnd + 1, "verification_results": results}, files)
     return path
 
 
