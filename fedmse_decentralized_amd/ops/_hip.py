@@ -54,7 +54,6 @@ AUC_DTYPE = np.dtype([
 ])
 SEG_DTYPE = np.dtype([("sse", "<u8"), ("n", "<i4"), ("batch", "<i4"), ("out", "<u8")])
 
-FWD_ROWS_PER_BLOCK = 256   # 4 waves x 4 tiles of 16 rows
 
 
 class TrainArgs(ctypes.Structure):
@@ -200,20 +199,39 @@ class on_stream:
 
 
 # ---------------------------------------------------------------------------
+FWD_BLOCK_SLOTS = 4 * 256   # resident fwd_rows workgroups on an MI355X (40 KB LDS each, 4 per CU, 256 CUs)
+
+
+def fwd_rows_per_block(total_rows: int, n_items: int) -> int:
+    """Rows per fwd_rows workgroup (multiple of 64): as many workgroups as
+    the chip holds at once, never a sliver of a second wave of them — a
+    5 x 52,800-row dev-set scoring at 256 rows per block is 1,035 blocks,
+    11 of which would run alone after the first 1,024."""
+    fixed = int(os.environ.get("FEDMX_FWD_ROWS_PER_BLOCK", "0"))   # A/B override
+    if fixed > 0:
+        return fixed
+    slots = max(FWD_BLOCK_SLOTS - n_items, 1)
+    per = -(-int(total_rows) // slots)
+    per = max(64, -(-per // 64) * 64)
+    return int(per)
+
+
 def build_fwd_desc(param_ptrs: np.ndarray, x_ptrs: np.ndarray, nrows: np.ndarray, sse_ptrs: np.ndarray,
-                   lat_ptrs: np.ndarray, dims) -> np.ndarray:
-    """Vectorised FwdDesc construction: split items into <=256-row blocks."""
+                   lat_ptrs: np.ndarray, dims, rows_per_block: Optional[int] = None) -> np.ndarray:
+    """Vectorised FwdDesc construction: split items into row blocks (the
+    kernel loops over any block length in 16-row tiles)."""
     nrows = np.asarray(nrows, dtype=np.int64)
-    nblk = (nrows + FWD_ROWS_PER_BLOCK - 1) // FWD_ROWS_PER_BLOCK
+    rpb = rows_per_block or fwd_rows_per_block(int(nrows.sum()), len(nrows))
+    nblk = (nrows + rpb - 1) // rpb
     item = np.repeat(np.arange(len(nrows)), nblk)
     first = np.repeat(np.cumsum(nblk) - nblk, nblk)
-    r0 = (np.arange(int(nblk.sum())) - first) * FWD_ROWS_PER_BLOCK
+    r0 = (np.arange(int(nblk.sum())) - first) * rpb
     desc = np.zeros(len(item), dtype=FWD_DTYPE)
     desc["params"] = param_ptrs[item]
     desc["x"] = x_ptrs[item] + (4 * 128) * r0
     desc["sse"] = np.where(sse_ptrs[item] != 0, sse_ptrs[item] + 4 * r0, 0)
     desc["lat"] = np.where(lat_ptrs[item] != 0, lat_ptrs[item] + 4 * dims.latent * r0, 0)
-    desc["nrows"] = np.minimum(FWD_ROWS_PER_BLOCK, nrows[item] - r0)
+    desc["nrows"] = np.minimum(rpb, nrows[item] - r0)
     desc["lat_stride"] = dims.latent
     desc["d_in"] = dims.d_in
     desc["latent"] = dims.latent

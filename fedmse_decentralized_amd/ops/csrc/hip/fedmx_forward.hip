@@ -71,16 +71,26 @@ __global__ __launch_bounds__(256) void fwd_rows_kernel(const FwdDesc* __restrict
   const int g = lane >> 4;  // lane group: k sub-index / D row quad
   const int ntiles = (d.nrows + 15) >> 4;
 
+  // X[row][16u + 4g + j] for u = 0..7 : the lane's B-operand values for layer 1
+  // (k-step s = 4u + j supplies k = 16u + 4g + j) and its reference values for
+  // the layer-4 output rows it holds (Y^T[16u + 4g + j][row]).  The next
+  // tile's rows are loaded while this one computes (one tile ahead).
+  auto load_tile = [&](int tile, f32x4 (&xt)[8]) {
+    const int row = tile * 16 + c;
+    const int rr = row < d.nrows ? row : 0;   // padding rows: any valid row, masked at the end
+    const float* xr = d.x + (size_t)rr * DP + 4 * g;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xt[u] = *reinterpret_cast<const f32x4*>(xr + 16 * u);
+  };
+  f32x4 xn[8];
+  if (wave < ntiles) load_tile(wave, xn);
   for (int tile = wave; tile < ntiles; tile += 4) {
     const int row = tile * 16 + c;
     const bool valid = row < d.nrows;
-    // X[row][16u + 4g + j] for u = 0..7 : the lane's B-operand values for layer 1
-    // (k-step s = 4u + j supplies k = 16u + 4g + j) and its reference values for
-    // the layer-4 output rows it holds (Y^T[16u + 4g + j][row]).
     f32x4 x[8];
-    const float* xr = d.x + (size_t)row * DP + 4 * g;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) x[u] = valid ? *reinterpret_cast<const f32x4*>(xr + 16 * u) : zero4();
+    for (int u = 0; u < 8; ++u) x[u] = xn[u];
+    if (tile + 4 < ntiles) load_tile(tile + 4, xn);
     if (g == 3) x[7][3] = 1.0f;  // column DP-1 feeds the b1 column of W1a
 
     // ---- layer 1: H1^T[h][b] = sum_d W1a[h][d] X^T[d][b]
