@@ -218,3 +218,42 @@ def test_train8_kernel_matches_torch_engine(lam, mu):
     torch.testing.assert_close(hip.store.params.cpu(), ref.store.params, rtol=2e-3, atol=2e-5)
     torch.testing.assert_close(hip.store.best.cpu(), ref.store.best, rtol=2e-3, atol=2e-5)
     assert torch.equal(hip.store.adam_step.cpu(), ref.store.adam_step)
+
+
+def test_copy_rows_gather_scatter():
+    """Row copies through mapped index arrays (multi-rank exchange packing)."""
+    rt = _hip.runtime(DEV)
+    src = torch.randn(9, 40, device=DEV)
+    dst = torch.zeros(6, 40, device=DEV)
+    sidx, didx = rt.desc.put(np.array([8, 0, 3], dtype=np.int32), np.array([5, 1, 2], dtype=np.int32))
+    _hip.copy_rows(dst.data_ptr(), 40, didx, src.data_ptr(), 40, sidx, 3, 40, DEV)
+    # identity destination, row length shorter than the stride
+    dst2 = torch.zeros(3, 40, device=DEV)
+    _hip.copy_rows(dst2.data_ptr(), 40, 0, src.data_ptr(), 40, sidx, 3, 16, DEV)
+    torch.cuda.synchronize()
+    ref = torch.zeros(6, 40)
+    ref[5], ref[1], ref[2] = src[8].cpu(), src[0].cpu(), src[3].cpu()
+    assert torch.equal(dst.cpu(), ref)
+    assert torch.equal(dst2[:, :16].cpu(), src[[8, 0, 3], :16].cpu())
+    assert torch.count_nonzero(dst2[:, 16:]) == 0
+
+
+def test_forward_rows_independent_of_block_length():
+    params, _ = init_client_params(2, 3)
+    pad = canonical_to_padded(params).to(DEV)
+    x = _data(1000, seed=9).to(DEV)
+    outs = []
+    for rpb in (64, 256, 1024):
+        desc = _hip.build_fwd_desc(pad.data_ptr() + 4 * P_PAD * np.array([0, 1]), np.array([x.data_ptr()] * 2),
+                                   np.array([1000, 700]), np.zeros(2, np.int64), np.zeros(2, np.int64),
+                                   DEFAULT_DIMS, rows_per_block=rpb)
+        assert desc["nrows"].max() <= rpb
+    sse_a, _ = _hip.forward_rows(pad, [(0, x), (1, x[:700])], DEFAULT_DIMS, True, False)
+    import os
+    os.environ["FEDMX_FWD_ROWS_PER_BLOCK"] = "64"
+    try:
+        sse_b, _ = _hip.forward_rows(pad, [(0, x), (1, x[:700])], DEFAULT_DIMS, True, False)
+    finally:
+        del os.environ["FEDMX_FWD_ROWS_PER_BLOCK"]
+    for a, b in zip(sse_a, sse_b):
+        assert torch.equal(a, b)

@@ -74,3 +74,15 @@ def test_dims_limits():
     with pytest.raises(ValueError):
         ModelDims(128, 27, 7)
     ModelDims(46, 27, 7)  # CIC-style feature count is supported
+
+
+def test_fwd_rows_per_block_fills_the_chip_without_a_straggler_wave():
+    from fedmse_decentralized_amd.ops._hip import FWD_BLOCK_SLOTS, fwd_rows_per_block
+
+    for total, items in ((5 * 52800, 5), (5 * 6600, 5), (10 * 3900, 10), (128 * 169000, 128), (17, 1)):
+        rpb = fwd_rows_per_block(total, items)
+        assert rpb % 64 == 0 and rpb >= 64
+        per_item = [total // items] * items
+        blocks = sum(-(-n // rpb) for n in per_item)
+        if rpb > 64:
+            assert blocks <= FWD_BLOCK_SLOTS
