@@ -157,6 +157,11 @@ class DeviceRound:
         if fed.local:
             self.vsse_off = torch.from_numpy(self.vplan.offs.astype(np.int32)).to(dev)
             self.vsse_n = torch.from_numpy(self.vplan.sizes.astype(np.int32)).to(dev)
+            # fused verification (one launch: forward + decide/adopt + snapshots)
+            # when every receiver's verification rows fit the kernel's LDS buffer
+            self._vdata = vdata
+            self.vx = torch.tensor([d.data_ptr() for d in vdata], dtype=torch.int64, device=dev)
+        self.fused_verify = bool(fed.local) and max(int(d.shape[0]) for d in vdata) <= _hip.VERIFY_MAX_ROWS
         self.rule = 1 if fed.update_type == "mse_avg" else 0
         self.pending: deque = deque()
         self.all_rounds: Dict[int, dict] = {}
@@ -276,7 +281,7 @@ class DeviceRound:
             # one kernel reduces MSE + drift, decides, adopts and bumps the cap
             # count; rejected counts go straight into the side stream's report
             # buffer ([AUCs | rejected])
-            if self.n_local:
+            if self.n_local and not self.fused_verify:
                 self.vplan.run()
             d = _hip.DecideArgs(params=st.params.data_ptr(), anchor=st.anchor.data_ptr(),
                                 hist=self.hist.data_ptr(), agg=self.agg.data_ptr(), state=self.state.data_ptr(),
@@ -288,14 +293,24 @@ class DeviceRound:
                                 rejected=self.rejected.data_ptr(), rej_out=self.side_rep.data_ptr() + 8 * N,
                                 thr=float(cfg.verification_threshold), pthr=float(cfg.performance_threshold),
                                 start=self.start, n_local=self.n_local, P=P_PAD, d_in=fed.dims.d_in)
-            _hip.decide_adopt(d, dev)
+            if self.fused_verify:
+                # verification forward, decisions, adoption and the evaluation /
+                # artefact snapshots in one launch (bit-identical to the
+                # separate kernels below)
+                v = _hip.VerifyArgs(D=d, vx=self.vx.data_ptr(), vn=self.vsse_n.data_ptr(),
+                                    eval_params=self.eval_params.data_ptr(), best_stage=self.best_stage.data_ptr(),
+                                    best=st.best.data_ptr(), latent=fed.dims.latent, hidden=fed.dims.hidden)
+                _hip.verify_decide(v, dev)
+            else:
+                _hip.decide_adopt(d, dev)
         slot_ptr, slot = self.rt.out.take(np.float64, 2 * N)
-        # snapshot params (for the evaluation) and the best models (for the
-        # artefacts) on the main stream: one fused device copy, so the next
-        # round's training can start right away
-        nd = st.params.numel() // 2
-        _hip.copy2_f64(self.eval_params.data_ptr(), st.params.data_ptr(), nd,
-                       self.best_stage.data_ptr(), st.best.data_ptr(), nd, dev)
+        if not self.fused_verify:
+            # snapshot params (for the evaluation) and the best models (for the
+            # artefacts) on the main stream: one fused device copy, so the next
+            # round's training can start right away
+            nd = st.params.numel() // 2
+            _hip.copy2_f64(self.eval_params.data_ptr(), st.params.data_ptr(), nd,
+                           self.best_stage.data_ptr(), st.best.data_ptr(), nd, dev)
         ev_dec = torch.cuda.Event()
         ev_dec.record()
         with tel.phase("eval"), _hip.on_stream(self.side):

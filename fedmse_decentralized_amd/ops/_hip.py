@@ -92,6 +92,14 @@ class DecideArgs(ctypes.Structure):
                 ("P", _i32), ("d_in", _i32)]
 
 
+VERIFY_MAX_ROWS = 4096   # rows of one receiver's verification data the fused kernel keeps in LDS
+
+
+class VerifyArgs(ctypes.Structure):
+    _fields_ = [("D", DecideArgs), ("vx", _vp), ("vn", _vp), ("eval_params", _vp), ("best_stage", _vp),
+                ("best", _vp), ("latent", _i32), ("hidden", _i32)]
+
+
 def lib():
     global _lib
     if _lib is not None:
@@ -118,6 +126,7 @@ def lib():
                 "fedmx_probe_mfma": [vp, vp],
                 "fedmx_elect_wsum": [ctypes.POINTER(ElectArgs), ctypes.POINTER(WsumArgs), vp],
                 "fedmx_decide_adopt": [ctypes.POINTER(DecideArgs), vp],
+                "fedmx_verify_decide": [ctypes.POINTER(VerifyArgs), vp],
                 "fedmx_copy_f64": [vp, vp, i32, vp],
                 "fedmx_copy2_f64": [vp, vp, i32, vp, vp, i32, vp],
                 "fedmx_copy_rows": [vp, i32, vp, vp, i32, vp, i32, i32, vp],
@@ -132,9 +141,10 @@ def lib():
             assert L.fedmx_auc_desc_size() == AUC_DTYPE.itemsize
             assert L.fedmx_seg_desc_size() == SEG_DTYPE.itemsize
             assert L.fedmx_train_args_size() == ctypes.sizeof(TrainArgs)
-            sz = (ctypes.c_int * 3)()
+            sz = (ctypes.c_int * 4)()
             L.fedmx_protocol_sizes(ctypes.cast(sz, ctypes.c_void_p))
-            assert tuple(sz) == (ctypes.sizeof(ElectArgs), ctypes.sizeof(WsumArgs), ctypes.sizeof(DecideArgs)), tuple(sz)
+            assert tuple(sz) == (ctypes.sizeof(ElectArgs), ctypes.sizeof(WsumArgs), ctypes.sizeof(DecideArgs),
+                                 ctypes.sizeof(VerifyArgs)), tuple(sz)
             _lib = L
     return _lib
 
@@ -417,6 +427,11 @@ def elect_wsum(eargs: ElectArgs, wargs: WsumArgs, device):
 
 def decide_adopt(args: DecideArgs, device):
     _check(lib().fedmx_decide_adopt(ctypes.byref(args), _stream(device)), "fedmx_decide_adopt")
+
+
+def verify_decide(args: VerifyArgs, device):
+    """Verification forward + decide_adopt + evaluation snapshot, one launch."""
+    _check(lib().fedmx_verify_decide(ctypes.byref(args), _stream(device)), "fedmx_verify_decide")
 
 
 def copy_f64(dst_ptr: int, src_ptr: int, n: int, device):

@@ -18,9 +18,14 @@
 //                          the aggregate and re-anchor FedProx, the history is
 //                          always the last received aggregate; the aggregator
 //                          itself loads the aggregate without re-anchoring
+//  * verify_decide_kernel: the verification forward of the aggregate on each
+//                          hosted receiver's data, decide_adopt and the
+//                          evaluation snapshot in ONE launch (a workgroup per
+//                          receiver: its rows fit one block, so no cross-block
+//                          step); bit-identical to fwd_rows + decide_adopt + copy
 //  * copy_f64_kernel     : device -> mapped host report slots
 // Every kernel is a no-op when the election found no aggregator.
-#include "fedmx_common.h"
+#include "fedmx_forward_common.h"
 
 namespace fedmx {
 
@@ -304,6 +309,160 @@ __global__ __launch_bounds__(1024) void decide_adopt_kernel(const DecideArgs A) 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused verification: per hosted client one 512-thread workgroup stages the
+// aggregate, runs the shared batched forward (fwd_rows_block, 8 waves) over
+// its verification rows into LDS, then does decide_adopt's work with the same
+// reductions (MSE: 256-thread strided sum; drift: each thread plays two of
+// decide_adopt's 1024 threads, partial sums combined in the same order) and
+// writes the evaluation / artefact snapshots of its rows in the same pass.
+// (512 threads: the forward keeps its registers — at 1024 it spilled.)
+constexpr int VERIFY_MAX_ROWS = 4096;
+
+struct VerifyArgs {
+  DecideArgs D;               // sse / sse_off / sse_n unused
+  const int64_t* vx;          // [n_local] address of each receiver's verification rows [n, DP]
+  const int32_t* vn;          // [n_local] their row counts (<= VERIFY_MAX_ROWS)
+  float* eval_params;         // [n_local, P] parameter snapshot for the side-stream evaluation
+  float* best_stage;          // [n_local, P] best-model snapshot for the artefact writer
+  const float* best;          // [n_local, P]
+  int32_t latent, hidden;
+};
+static_assert(sizeof(VerifyArgs) == sizeof(DecideArgs) + 48, "VerifyArgs layout is shared with Python");
+
+__global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) {
+  const DecideArgs& A = V.D;
+  __shared__ __attribute__((aligned(16))) float sW1[HP * S_W1];
+  __shared__ __attribute__((aligned(16))) float sW2[ZP * S_W2];
+  __shared__ __attribute__((aligned(16))) float sW3[HP * S_W3];
+  __shared__ __attribute__((aligned(16))) float sW4[DP * S_W4];
+  __shared__ float s_sse[VERIFY_MAX_ROWS];
+  __shared__ int s_ok;
+  __shared__ double s_d[4];
+  __shared__ float part[8][16];
+  const int a = A.state[0];
+  if (a >= 0 && blockIdx.x == 0 && threadIdx.x == 0) A.agg_counts[a] += 1;
+  const int cl = blockIdx.x;
+  if (cl >= A.n_local) return;
+  const int c = A.start + cl;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const size_t off = (size_t)cl * A.P;
+  const int n4 = A.P / 4;
+  const f32x4* src = reinterpret_cast<const f32x4*>(A.agg);
+  f32x4* prm = reinterpret_cast<f32x4*>(A.params + off);
+  f32x4* evp = reinterpret_cast<f32x4*>(V.eval_params + off);
+  f32x4* bst = reinterpret_cast<f32x4*>(V.best_stage + off);
+  const f32x4* bsrc = reinterpret_cast<const f32x4*>(V.best + off);
+  bool ok = false, load = false;
+  if (a >= 0 && c == a) {
+    load = true;   // the aggregator loads its aggregate (anchor / history unchanged)
+  } else if (a >= 0) {
+    const int had_hist = A.has_hist[cl];
+    // ---- SSE rows of the aggregate on this receiver's data (fwd_rows arithmetic)
+    stage_params(A.agg, sW1, sW2, sW3, sW4);
+    __syncthreads();
+    FwdDesc d;
+    d.params = A.agg;
+    d.x = reinterpret_cast<const float*>(V.vx[cl]);
+    d.sse = s_sse;
+    d.lat = nullptr;
+    d.nrows = V.vn[cl];
+    d.lat_stride = V.latent;
+    d.d_in = A.d_in;
+    d.latent = V.latent;
+    d.hidden = V.hidden;
+    fwd_rows_block(d, sW1, sW2, sW3, sW4, wv, 8, s_sse);
+    __syncthreads();
+    // ---- MSE (score_reduce / decide_adopt order)
+    double mse;
+    {
+      const int n = d.nrows;
+      double sv = 0.0;
+      if (tid < 256) {
+#pragma unroll 8
+        for (int r = tid; r < n; r += 256) sv += (double)s_sse[r];
+      }
+      for (int o = 32; o >= 1; o >>= 1) sv += __shfl_xor(sv, o, 64);
+      if (lane == 0 && wv < 4) s_d[wv] = sv;
+      __syncthreads();
+      const double tot = s_d[0] + s_d[1] + s_d[2] + s_d[3];
+      mse = n > 0 ? tot / ((double)n * A.d_in) : __builtin_nan("");
+    }
+    // ---- drift of the receiver's history vs the aggregate (param_drift order)
+    float drift = 0.f;
+    if (had_hist) {
+      // virtual threads vt = tid and tid + 512 of a 1024-thread block
+      const float* h = A.hist + off;
+      float acc[2][8];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[q][t] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        for (int p = tid + 512 * q; p < A.P; p += 1024) {
+          const int sg = A.seg[p];
+          const float df = h[p] - A.agg[p];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) acc[q][t] += (sg == t) ? df * df : 0.0f;
+        }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const float v = wave_sum(acc[q][t]);
+          if (lane == 0) part[t][wv + 8 * q] = v;
+        }
+      __syncthreads();
+      if (tid == 0) {
+        float tot = 0.f;
+        for (int t = 0; t < 8; ++t) {
+          float s2 = 0.f;
+          for (int w = 0; w < 16; ++w) s2 += part[t][w];
+          tot += sqrtf(s2);
+        }
+        drift = tot;
+      }
+    }
+    if (tid == 0) {
+      const double perf = 1.0 / (1.0 + mse);
+      int okk;
+      if (!had_hist) {
+        okk = 1;  // the first received model is accepted unconditionally
+        A.has_hist[cl] = 1;
+      } else {
+        const double change = perf - A.hist_perf[cl];
+        okk = ((double)drift <= A.thr) && (change >= -A.pthr);
+      }
+      A.hist_perf[cl] = perf;
+      const int rj = okk ? 0 : A.rejected[cl] + 1;
+      A.rejected[cl] = rj;
+      A.rej_out[c] = (double)rj;
+      s_ok = okk;
+    }
+    __syncthreads();
+    ok = s_ok != 0;
+    load = ok;
+  }
+  // ---- adoption + history + snapshots in one pass over the row
+  const bool receiver = a >= 0 && c != a;
+  for (int i = tid; i < n4; i += blockDim.x) {
+    const f32x4 v = src[i];
+    f32x4 p;
+    if (load) {
+      p = v;
+      prm[i] = v;
+      if (ok) reinterpret_cast<f32x4*>(A.anchor + off)[i] = v;
+    } else {
+      p = prm[i];
+    }
+    if (receiver) reinterpret_cast<f32x4*>(A.hist + off)[i] = v;
+    evp[i] = p;
+    bst[i] = bsrc[i];
+  }
+}
+
 __global__ __launch_bounds__(256) void copy_f64_kernel(double* __restrict__ dst, const double* __restrict__ src,
                                                        int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -375,6 +534,13 @@ int fedmx_elect_wsum(const void* eargs, const void* wargs, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+int fedmx_verify_decide(const void* args, hipStream_t stream) {
+  const fedmx::VerifyArgs& V = *reinterpret_cast<const fedmx::VerifyArgs*>(args);
+  if (V.D.P % 4 != 0 || V.D.P != fedmx::P_PAD) return -1;
+  hipLaunchKernelGGL(fedmx::verify_decide_kernel, dim3(V.D.n_local > 0 ? V.D.n_local : 1), dim3(512), 0, stream, V);
+  return (int)hipGetLastError();
+}
+
 int fedmx_copy_f64(double* dst, const double* src, int n, hipStream_t stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(fedmx::copy_f64_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, dst, src, n);
@@ -385,6 +551,7 @@ int fedmx_protocol_sizes(int* out) {
   out[0] = (int)sizeof(fedmx::ElectArgs);
   out[1] = (int)sizeof(fedmx::WsumArgs);
   out[2] = (int)sizeof(fedmx::DecideArgs);
+  out[3] = (int)sizeof(fedmx::VerifyArgs);
   return 0;
 }
 
