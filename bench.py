@@ -67,6 +67,9 @@ def main(argv=None):
     p.add_argument("--trace", default=None, help="per-phase JSONL trace (adds device syncs)")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
     p.add_argument("--profile", default=None, help="cProfile the timed rounds (rank 0) into this file")
+    p.add_argument("--phantom-ranks", type=int, default=0,
+                   help="projection on ONE GPU: run rank 0 of a W-rank weak-scaling job with the collectives "
+                        "stubbed out (parallel.comm.PhantomComm); the record is labelled as a projection")
     args = p.parse_args(argv)
 
     from fedmse_decentralized_amd.config import ExperimentConfig
@@ -76,7 +79,12 @@ def main(argv=None):
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     device = "cuda" if torch.cuda.is_available() else "cpu"
-    comm = init_comm(device=device)
+    if args.phantom_ranks > 1:
+        from fedmse_decentralized_amd.parallel.comm import PhantomComm
+
+        comm = PhantomComm(args.phantom_ranks, device)
+    else:
+        comm = init_comm(device=device)
     setup_logging("WARNING", rank=comm.rank)
     n_gpus = comm.world_size
     if args.gpus != n_gpus and comm.is_root:
@@ -92,6 +100,9 @@ def main(argv=None):
         trace_file=args.trace, log_level="WARNING")
     fed = Federation(cfg, args.model_type, args.update_type, run=0, comm=comm,
                      write_reports=not args.no_artifacts).setup()
+    if args.phantom_ranks > 1 and fed._fast is None:
+        # the host protocol reads other ranks' vote records, which a phantom job does not have
+        raise SystemExit("--phantom-ranks needs the device-resident round protocol (HIP engine, compat fixed)")
 
     def one_round():
         if fed.round_idx and fed.round_idx % EPISODE == 0:
@@ -171,6 +182,9 @@ def main(argv=None):
             "phase_ms_total": {k: round(v, 3) for k, v in fed.tel.summary().items()},
             "writer_busy_ms_per_round": round(1e3 * (fed.writer.busy_s - w_busy0) / args.steps, 4),
         }
+        if args.phantom_ranks > 1:
+            rec["projection"] = (f"rank 0 of a {args.phantom_ranks}-rank job on ONE GPU, collectives stubbed "
+                                 "(no RCCL time); value assumes every rank is as fast as this one")
         line = json.dumps(rec)
         print(line, flush=True)
         if args.out:

@@ -248,6 +248,12 @@ class DeviceRound:
                                    P_PAD, dev)
                     # vote records: 4 doubles = 8 floats per client, packed into the tail row
                     _hip.copy_rows(send[slots].data_ptr(), 8, 0, self.vec.data_ptr(), 8, cid_ptr, len(mine), 8, dev)
+                    if comm.phantom and len(mine) < slots:
+                        # single-GPU projection (PhantomComm): other ranks' rows are
+                        # copies of this rank's, so the spare slots must hold real models
+                        n = len(mine)
+                        send[n:slots].copy_(send[:1].expand(slots - n, P_PAD))
+                        send[slots, 8 * n:8 * slots].copy_(send[slots, :8].repeat(slots - n))
                 allg = comm.all_gather(send).reshape(-1, P_PAD)          # [world * (slots+1), P]
                 owners = [fed.shard.owner(c) for c in selected]
                 # record of client c: tail row of its owner, entry j (8-float units)
@@ -260,7 +266,7 @@ class DeviceRound:
                                   dtype=np.int64)
                 rec["_keep"] = (allg, send)
         with tel.phase("aggregate"):
-            noise = np.array([fed.noise.rand() for _ in range(k * (k - 1))], dtype=np.float64)
+            noise = np.asarray(fed.noise.rand_n(k * (k - 1)), dtype=np.float64)
             sel_ptr, noise_ptr, rows_ptr = self.rt.desc.put(np.asarray(selected, dtype=np.int32),
                                                             noise if noise.size else np.zeros(1), rows)
             rep_ptr, rep_view = self.rt.out.take(np.int32, 2)

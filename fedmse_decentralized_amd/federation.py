@@ -373,7 +373,7 @@ class Federation:
                 # one k x (k-1) table per round, drawn whatever the outcome (the
                 # device protocol draws the same table)
                 k = len(selected)
-                noise = _TableNoise([self.noise.rand() for _ in range(k * (k - 1))])
+                noise = _TableNoise([float(u) for u in self.noise.rand_n(k * (k - 1))])
             el = elect(selected, base_scores, self.agg_counts, cfg.max_aggregation, noise,
                        log_enabled=info, vote_mse_cap=cap, fallback_rng=self.fallback_rng)
             aggregator = el.aggregator

@@ -60,16 +60,19 @@ static_assert(sizeof(WsumArgs) == 48, "WsumArgs layout is shared with Python");
 // after every workgroup here has read the counts).
 __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, const WsumArgs W) {
   __shared__ float s_w[1024];
+  __shared__ int64_t s_rows[1024];
   __shared__ int s_agg;
   const int tid = threadIdx.x;
+  // the source rows live in the mapped descriptor ring (host memory): one
+  // parallel load here instead of one dependent PCIe round trip per row below
+  for (int j = tid; j < W.k; j += blockDim.x) s_rows[j] = W.rows[j];
   if (E.k <= 64) {
     // Small selections (every reference config): wave 0 stages the inputs
-    // with one parallel load each (the noise table lives in mapped host
-    // memory: one PCIe round trip instead of one per draw); each candidate
-    // lane forms its noisy score, then the reference's serial first-minimum
-    // scan runs over the lanes.  Same double arithmetic as the serial loop
-    // below (bit-identical decisions).
-    __shared__ double s_noise[64 * 63];
+    // with one parallel load each; each candidate lane forms its noisy score
+    // with the current voter's noise row (mapped host memory: one PCIe round
+    // trip per voter tried, normally just the first), then the reference's
+    // serial first-minimum scan runs over the lanes.  Same double arithmetic
+    // as the serial loop below (bit-identical decisions).
     __shared__ double s_inv[64];
     if (tid < 64) {
       const int lane = tid;
@@ -82,10 +85,6 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
         mse = E.vec[(size_t)c * 4 + 3];
         cnt = E.agg_counts[c];
       }
-      for (int i = lane; i < k * (k - 1); i += 64) s_noise[i] = E.noise[i];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       int agg = -1, voter = -1;
       for (int vi = 0; vi < k && agg < 0; ++vi) {
         const int v = __shfl(c, vi, 64);
@@ -93,7 +92,7 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
         bool cand = lane < k && lane != vi && cnt < E.cap;
         double sc = 0.0;
         if (lane < k && lane != vi) {
-          const double f = 1.0 + (s_noise[(size_t)vi * (k - 1) + lane - (lane > vi ? 1 : 0)] - 0.5) * 0.0002;
+          const double f = 1.0 + (E.noise[(size_t)vi * (k - 1) + lane - (lane > vi ? 1 : 0)] - 0.5) * 0.0002;
           sc = vs * f;
         }
         // the serial scan of the reference loop over the candidates' lanes
@@ -181,12 +180,24 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
   if (s_agg < 0) return;
   const int i = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= W.P) return;
+  // eight independent row loads in flight, added strictly in selection order
+  // (the separately rounded fp32 order of weighted_sum_kernel)
   f32x4 acc = zero4();
-  for (int k = 0; k < W.k; ++k) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(W.base + (size_t)W.rows[k] * W.P + i);
-    const float wk = s_w[k];
+  constexpr int U = 8;
+  for (int k0 = 0; k0 < W.k; k0 += U) {
+    f32x4 v[U];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc[r] = (k == 0) ? __fmul_rn(v[r], wk) : __fadd_rn(acc[r], __fmul_rn(v[r], wk));
+    for (int u = 0; u < U; ++u)
+      if (k0 + u < W.k) v[u] = *reinterpret_cast<const f32x4*>(W.base + (size_t)s_rows[k0 + u] * W.P + i);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (k0 + u < W.k) {
+        const float wk = s_w[k0 + u];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[r] = (k0 + u == 0) ? __fmul_rn(v[u][r], wk) : __fadd_rn(acc[r], __fmul_rn(v[u][r], wk));
+      }
+    }
   }
   *reinterpret_cast<f32x4*>(W.out + i) = acc;
 }

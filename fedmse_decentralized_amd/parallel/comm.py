@@ -34,6 +34,7 @@ class Comm:
     rank: int = 0
     world_size: int = 1
     device: torch.device = torch.device("cpu")
+    phantom: bool = False   # PhantomComm: collectives stubbed (single-GPU projection)
 
     @property
     def is_root(self) -> bool:
@@ -92,6 +93,43 @@ class LoopbackComm(Comm):
 
     def all_gather_object(self, obj):
         return [obj]
+
+    def all_reduce_inplace(self, t):
+        pass
+
+
+class PhantomComm(Comm):
+    """Rank 0 of a ``world``-rank job with the collectives stubbed out locally:
+    ``all_gather`` repeats this rank's contribution for every rank and the
+    all-reduces leave the local values as they are.
+
+    A single-GPU *projection* tool (``bench.py --phantom-ranks W``): the rank
+    does exactly the per-rank GPU and host work of a W-GPU weak-scaling job
+    (its 10 clients, the W-times larger replicated dev set and vote data, the
+    W-rank packing / unpacking of the exchange) without RCCL, so the per-rank
+    round time of the 8-GPU job can be measured, and optimised, on one GPU.
+    The numbers it produces (AUCs, decisions) are not a federation's."""
+
+    phantom = True
+
+    def __init__(self, world: int, device: Optional[torch.device] = None):
+        self.rank = 0
+        self.world_size = int(world)
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+
+    @_np_wrap
+    def all_reduce_sum(self, t):
+        return t
+
+    def all_gather(self, t):
+        x = t if isinstance(t, torch.Tensor) else torch.as_tensor(t)
+        return x.unsqueeze(0).expand((self.world_size,) + tuple(x.shape)).contiguous()
+
+    def broadcast(self, t, src):
+        return t
+
+    def all_gather_object(self, obj):
+        return [obj] * self.world_size
 
     def all_reduce_inplace(self, t):
         pass

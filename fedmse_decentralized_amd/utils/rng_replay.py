@@ -51,6 +51,11 @@ class TorchRngReplay:
         self._run(f)
         self.draws += int(n)
 
+    def rand_n(self, n: int):
+        import numpy as np
+
+        return np.array([self.rand() for _ in range(n)], dtype=np.float64)
+
     def rand(self) -> float:
         self.draws += 1
         return float(self._run(lambda: torch.rand(1).item()))
@@ -83,3 +88,9 @@ class HostNoise:
 
     def rand(self) -> float:
         return float(self.rng.random())
+
+    def rand_n(self, n: int):
+        """``n`` draws at once: the same values, in the same order, as ``n``
+        calls of :meth:`rand` (one vectorised call: the k(k-1) election draws
+        of an 80-client round cost 0.6 ms of host time one by one)."""
+        return self.rng.random(n)

@@ -148,3 +148,18 @@ def test_device_round_is_deterministic(tmp_path):
     assert a == b
     for name in ("params", "adam_m", "adam_v", "anchor", "best"):
         assert torch.equal(getattr(fa.engine.store, name), getattr(fb.engine.store, name)), name
+
+
+def test_bench_phantom_ranks_projection(tmp_path):
+    """bench.py --phantom-ranks: rank 0 of a 4-rank weak-scaling job on one
+    GPU (40 clients, collectives stubbed) runs and labels its record."""
+    import json
+
+    import bench
+
+    out = tmp_path / "b.json"
+    assert bench.main(["--phantom-ranks", "4", "--steps", "3", "--warmup", "1", "--no-artifacts",
+                       "--out", str(out)]) == 0
+    rec = json.loads(out.read_text())
+    assert rec["config"]["clients"] == 40 and rec["config"]["device_protocol"]
+    assert "projection" in rec and rec["value"] > 0

@@ -126,3 +126,23 @@ def test_parallel_combos_two_ranks(tmp_path):
         got = json.load(open(os.path.join(out, f"combo_rank{r}.json")))
         assert got == ref
     assert os.path.exists(os.path.join(out, "Checkpoint", "Results", "Update", "4"))
+
+
+def test_phantom_comm_semantics():
+    """PhantomComm (single-GPU projection of rank 0 of a W-rank job): the
+    all-gather repeats the local contribution, all-reduces keep local values."""
+    from fedmse_decentralized_amd.parallel.comm import LoopbackComm, PhantomComm
+
+    c = PhantomComm(8)
+    assert c.world_size == 8 and c.rank == 0 and c.is_root and c.phantom
+    assert not LoopbackComm().phantom
+    x = torch.arange(6, dtype=torch.float32).reshape(3, 2)
+    g = c.all_gather(x)
+    assert g.shape == (8, 3, 2) and g.is_contiguous()
+    assert all(torch.equal(g[r], x) for r in range(8))
+    v = np.arange(4, dtype=np.float64)
+    np.testing.assert_array_equal(c.all_reduce_sum(v), v)
+    t = x.clone()
+    c.all_reduce_inplace(t)
+    assert torch.equal(t, x)
+    assert c.all_gather_object("h") == ["h"] * 8

@@ -174,3 +174,12 @@ def test_peer_api_roundtrip(tmp_path):
     assert out is not None and torch.equal(peers[1].params(), before)
     sd = peers[1].state_dict()
     assert list(sd)[0] == "encoder.encoder_network.0.weight"
+
+
+def test_host_noise_rand_n_matches_scalar_draws():
+    """The vectorised election-noise draw is the same stream as k(k-1) scalar
+    draws (the device round and the host round consume the same values)."""
+    a, b = HostNoise(123), HostNoise(123)
+    seq = [a.rand() for _ in range(40 * 39)] + [a.rand()]
+    vec = list(b.rand_n(40 * 39)) + [b.rand()]
+    assert seq == vec
