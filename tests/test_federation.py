@@ -231,3 +231,41 @@ def test_baseline_config1_reference_csvs_cpu(tmp_path):
     assert 0.5 < best["hybrid"]["avg"] <= 1.0
     summ = json.load(open(os.path.join(cfg.checkpoint_dir, "training_summary.json")))
     assert summ["best_metrics"]["hybrid"]["avg"] == best["hybrid"]["avg"]
+
+
+KITSUNE_IID = "/root/reference/Data/Kitsune-Network-Attack-Dataset/Client_Data_IID"
+RUN21_LOG = "/root/reference/src/run21.log"
+
+
+@pytest.mark.skipif(not (os.path.isdir(KITSUNE_IID) and os.path.exists(RUN21_LOG)), reason="reference data not mounted")
+def test_reference_compat_reproduces_shipped_run21_round1(tmp_path):
+    """The reference's shipped log (`src/run21.log`, Kitsune IID-10, seed
+    1234) replayed in reference-compat mode: round 1 of autoencoder + avg
+    gives the log's ten per-client AUCs (scripts/run21_parity.py)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    from run21_parity import parse_log
+
+    from fedmse_decentralized_amd import federation
+    from fedmse_decentralized_amd.federation import Federation
+
+    groups, _ = parse_log(RUN21_LOG)
+    dl = {"data_path": KITSUNE_IID, "devices_list": [
+        {"id": i, "name": f"Kitsune-Client-{i}", "normal_data_path": f"Client-{i}/normal",
+         "abnormal_data_path": f"Client-{i}/abnormal", "test_normal_data_path": f"Client-{i}/test_normal"}
+        for i in range(1, 11)]}
+    p = tmp_path / "k.json"
+    p.write_text(json.dumps(dl))
+    cfg = ExperimentConfig(config_file=str(p), network_size=10, num_participants=0.5, epoch=5, num_rounds=3,
+                           lr_rate=1e-3, shrink_lambda=5, batch_size=12, data_seed=1234, num_runs=1,
+                           model_types=["autoencoder"], update_types=["avg"], backend="torch", device="cpu",
+                           compat="reference", save_checkpoints=False, output_root=str(tmp_path),
+                           log_level="WARNING")
+    federation._PREP_CACHE.clear()
+    fed = Federation(cfg, "autoencoder", "avg", 0).setup()
+    r = fed.run_round()
+    fed.finish()
+    fed.writer.flush()
+    # autoencoder + avg is the log's 4th combination
+    np.testing.assert_allclose(np.asarray(r.metrics), groups[3][0], atol=1e-6)
