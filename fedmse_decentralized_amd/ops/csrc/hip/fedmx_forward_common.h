@@ -22,28 +22,43 @@ struct FwdDesc {
 };
 static_assert(sizeof(FwdDesc) == 64, "FwdDesc layout is shared with Python");
 
+__device__ __forceinline__ void stage_param4(float* sW1, float* sW2, float* sW3, float* sW4, int i, f32x4 v) {
+  int e = i * 4;
+  if (e < OFF_W2) {
+    int r = e / DP, c = e % DP;
+    lds_write4(&sW1[r * S_W1 + c], v);
+  } else if (e < OFF_W3) {
+    e -= OFF_W2;
+    int r = e / HP, c = e % HP;
+    lds_write4(&sW2[r * S_W2 + c], v);
+  } else if (e < OFF_W4) {
+    e -= OFF_W3;
+    int r = e / ZP, c = e % ZP;
+    lds_write4(&sW3[r * S_W3 + c], v);
+  } else {
+    e -= OFF_W4;
+    int r = e / HP, c = e % HP;
+    lds_write4(&sW4[r * S_W4 + c], v);
+  }
+}
+
+// The parameter vector (2,304 float4) is staged with all of a thread's
+// loads issued before its LDS writes: 2-3 global round trips per workgroup
+// instead of one per 256 / 512 elements.
 __device__ __forceinline__ void stage_params(const float* __restrict__ p, float* sW1, float* sW2, float* sW3,
                                              float* sW4) {
   const f32x4* p4 = reinterpret_cast<const f32x4*>(p);
-  for (int i = threadIdx.x; i < P_PAD / 4; i += blockDim.x) {
-    f32x4 v = p4[i];
-    int e = i * 4;
-    if (e < OFF_W2) {
-      int r = e / DP, c = e % DP;
-      lds_write4(&sW1[r * S_W1 + c], v);
-    } else if (e < OFF_W3) {
-      e -= OFF_W2;
-      int r = e / HP, c = e % HP;
-      lds_write4(&sW2[r * S_W2 + c], v);
-    } else if (e < OFF_W4) {
-      e -= OFF_W3;
-      int r = e / ZP, c = e % ZP;
-      lds_write4(&sW3[r * S_W3 + c], v);
-    } else {
-      e -= OFF_W4;
-      int r = e / HP, c = e % HP;
-      lds_write4(&sW4[r * S_W4 + c], v);
-    }
+  constexpr int N4 = P_PAD / 4;
+  constexpr int U = 4;
+  const int nt = blockDim.x;
+  for (int i0 = threadIdx.x; i0 < N4; i0 += U * nt) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * nt < N4) v[u] = p4[i0 + u * nt];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * nt < N4) stage_param4(sW1, sW2, sW3, sW4, i0 + u * nt, v[u]);
   }
 }
 

@@ -410,13 +410,26 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
       for (int q = 0; q < 2; ++q)
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[q][t] = 0.f;
+      // four p's loads in flight per step, accumulated in increasing p
 #pragma unroll
       for (int q = 0; q < 2; ++q)
-        for (int p = tid + 512 * q; p < A.P; p += 1024) {
-          const int sg = A.seg[p];
-          const float df = h[p] - A.agg[p];
+        for (int p0 = tid + 512 * q; p0 < A.P; p0 += 4096) {
+          int sg[4];
+          float df[4];
 #pragma unroll
-          for (int t = 0; t < 8; ++t) acc[q][t] += (sg == t) ? df * df : 0.0f;
+          for (int u = 0; u < 4; ++u) {
+            const int p = p0 + 1024 * u;
+            sg[u] = -1;
+            df[u] = 0.f;
+            if (p < A.P) {
+              sg[u] = A.seg[p];
+              df[u] = h[p] - A.agg[p];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc[q][t] += (sg[u] == t) ? df[u] * df[u] : 0.0f;
         }
 #pragma unroll
       for (int q = 0; q < 2; ++q)
@@ -458,19 +471,29 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
   }
   // ---- adoption + history + snapshots in one pass over the row
   const bool receiver = a >= 0 && c != a;
-  for (int i = tid; i < n4; i += blockDim.x) {
-    const f32x4 v = src[i];
-    f32x4 p;
-    if (load) {
-      p = v;
-      prm[i] = v;
-      if (ok) reinterpret_cast<f32x4*>(A.anchor + off)[i] = v;
-    } else {
-      p = prm[i];
+  constexpr int UA = (P_PAD / 4 + 511) / 512;   // every element of the row in one pass of loads
+  f32x4 v[UA], pv[UA], bv[UA];
+#pragma unroll
+  for (int u = 0; u < UA; ++u) {
+    const int i = tid + 512 * u;
+    if (i < n4) {
+      v[u] = src[i];
+      pv[u] = load ? v[u] : prm[i];
+      bv[u] = bsrc[i];
     }
-    if (receiver) reinterpret_cast<f32x4*>(A.hist + off)[i] = v;
-    evp[i] = p;
-    bst[i] = bsrc[i];
+  }
+#pragma unroll
+  for (int u = 0; u < UA; ++u) {
+    const int i = tid + 512 * u;
+    if (i < n4) {
+      if (load) {
+        prm[i] = v[u];
+        if (ok) reinterpret_cast<f32x4*>(A.anchor + off)[i] = v[u];
+      }
+      if (receiver) reinterpret_cast<f32x4*>(A.hist + off)[i] = v[u];
+      evp[i] = pv[u];
+      bst[i] = bv[u];
+    }
   }
 }
 
