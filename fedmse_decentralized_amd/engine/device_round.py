@@ -116,12 +116,20 @@ class DeviceRound:
         self.side = torch.cuda.Stream(device=dev)
         # [AUCs | rejected counts]; only hosted receivers' counts are ever
         # written, so other ranks' entries stay zero for the report all-reduce
-        self.side_rep = torch.zeros(2 * N, dtype=f64, device=dev)
-        self.eval_params = torch.empty_like(st.params)
-        self.best_stage = torch.empty_like(st.best)
-        self._ev_side_done = None
-        self.vs_bufs = [None, None]       # standardised vote data, by round parity
-        self._ev_vote = [None, None]
+        # The buffers the verification writes and the side stream reads
+        # (evaluation params, best-model stage, [AUCs | rejected]) rotate over
+        # NSIDE slots: round r reuses round r-NSIDE's, whose side work the host
+        # has normally collected already, so the main stream only waits (a
+        # cross-stream barrier packet, ~6 us on the chain) when it is not done.
+        NSIDE = 3
+        self.side_slots = [dict(rep=torch.zeros(2 * N, dtype=f64, device=dev),
+                                params=torch.empty_like(st.params), best=torch.empty_like(st.best), ev=None)
+                           for _ in range(NSIDE)]
+        # standardised vote data, by round parity.  Reuse needs no event of
+        # its own: round r+2's standardisation is queued on the side stream
+        # behind that stream's wait for round r+1's decisions, which the main
+        # stream records after round r's vote forward has read the buffer.
+        self.vs_bufs = [None, None]
         # best-model snapshots for the artefact writer: a ring of mapped host
         # slots filled by a device copy kernel (no torch pinned allocation or
         # blocking copy on the enqueue path); a slot is reused once the writer
@@ -197,8 +205,6 @@ class DeviceRound:
                                                device=dev)
             vs = self.vs_bufs[pb][:vdata.shape[0]]
             with _hip.on_stream(self.side):
-                if self._ev_vote[pb] is not None:   # round r-2's vote forward has read this buffer
-                    self.side.wait_event(self._ev_vote[pb])
                 _hip.standardize_ddof1(vdata.contiguous(), fed.dims.d_in, out=vs)
                 ev_std = torch.cuda.Event()
                 ev_std.record(self.side)
@@ -217,8 +223,6 @@ class DeviceRound:
                     outs += [self.vec[c].data_ptr() + 16 for c in local_sel]
                     batch += [0] * len(local_rows)
                 sse, _ = _hip.forward_rows(st.params, items, fed.dims, True, False)
-                self._ev_vote[pb] = torch.cuda.Event()
-                self._ev_vote[pb].record()
                 _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs)
         with tel.phase("comm"):
             if comm.world_size == 1:
@@ -280,8 +284,10 @@ class DeviceRound:
             _hip.elect_wsum(a, w, dev)
             rec["report"] = rep_view
         # the previous round's side work has read the snapshot / report buffers
-        if self._ev_side_done is not None:
-            torch.cuda.current_stream(dev).wait_event(self._ev_side_done)
+        side = self.side_slots[rnd % len(self.side_slots)]
+        if side["ev"] is not None and not side["ev"].query():
+            torch.cuda.current_stream(dev).wait_event(side["ev"])
+        side_rep, eval_params, best_stage = side["rep"], side["params"], side["best"]
         with tel.phase("verify"):
             # every hosted receiver: the aggregate's SSE rows on its data, then
             # one kernel reduces MSE + drift, decides, adopts and bumps the cap
@@ -296,7 +302,7 @@ class DeviceRound:
                                 sse_n=self.vsse_n.data_ptr() if self.n_local else 0,
                                 seg=eng._seg.data_ptr(), agg_counts=self.agg_counts.data_ptr(),
                                 has_hist=self.has_hist.data_ptr(), hist_perf=self.hist_perf.data_ptr(),
-                                rejected=self.rejected.data_ptr(), rej_out=self.side_rep.data_ptr() + 8 * N,
+                                rejected=self.rejected.data_ptr(), rej_out=side_rep.data_ptr() + 8 * N,
                                 thr=float(cfg.verification_threshold), pthr=float(cfg.performance_threshold),
                                 start=self.start, n_local=self.n_local, P=P_PAD, d_in=fed.dims.d_in)
             if self.fused_verify:
@@ -304,7 +310,7 @@ class DeviceRound:
                 # artefact snapshots in one launch (bit-identical to the
                 # separate kernels below)
                 v = _hip.VerifyArgs(D=d, vx=self.vx.data_ptr(), vn=self.vsse_n.data_ptr(),
-                                    eval_params=self.eval_params.data_ptr(), best_stage=self.best_stage.data_ptr(),
+                                    eval_params=eval_params.data_ptr(), best_stage=best_stage.data_ptr(),
                                     best=st.best.data_ptr(), latent=fed.dims.latent, hidden=fed.dims.hidden)
                 _hip.verify_decide(v, dev)
             else:
@@ -315,8 +321,8 @@ class DeviceRound:
             # artefacts) on the main stream: one fused device copy, so the next
             # round's training can start right away
             nd = st.params.numel() // 2
-            _hip.copy2_f64(self.eval_params.data_ptr(), st.params.data_ptr(), nd,
-                           self.best_stage.data_ptr(), st.best.data_ptr(), nd, dev)
+            _hip.copy2_f64(eval_params.data_ptr(), st.params.data_ptr(), nd,
+                           best_stage.data_ptr(), st.best.data_ptr(), nd, dev)
         ev_dec = torch.cuda.Event()
         ev_dec.record()
         with tel.phase("eval"), _hip.on_stream(self.side):
@@ -328,23 +334,23 @@ class DeviceRound:
                     self.snap_free[si].wait()
                 self.snap_free[si].clear()
                 nd = st.best.numel() // 2
-                _hip.copy2_f64(self.snap_buf.dev_ptr + si * st.best.numel() * 4, self.best_stage.data_ptr(), nd,
+                _hip.copy2_f64(self.snap_buf.dev_ptr + si * st.best.numel() * 4, best_stage.data_ptr(), nd,
                                0, 0, 0, dev)
                 rec["snap_slot"] = si
-            eng.evaluate_launch(fed.model_type, params=self.eval_params)
-            aucs_ptr = eng._plan(fed.model_type, self.eval_params)["aucs_buf"].dev_ptr
+            eng.evaluate_launch(fed.model_type, params=eval_params)
+            aucs_ptr = eng._plan(fed.model_type, eval_params)["aucs_buf"].dev_ptr
             if comm.world_size == 1:
-                _hip.copy2_f64(slot_ptr, aucs_ptr, N, slot_ptr + 8 * N, self.side_rep.data_ptr() + 8 * N, N, dev)
+                _hip.copy2_f64(slot_ptr, aucs_ptr, N, slot_ptr + 8 * N, side_rep.data_ptr() + 8 * N, N, dev)
             else:
                 # [AUCs | rejected counts]: one RCCL all-reduce, off the main stream
-                self.side_rep[:N].zero_()
+                side_rep[:N].zero_()
                 if self.n_local:
-                    _hip.copy_f64(self.side_rep.data_ptr() + 8 * self.start, aucs_ptr, self.n_local, dev)
-                comm.all_reduce_inplace(self.side_rep)
-                _hip.copy_f64(slot_ptr, self.side_rep.data_ptr(), 2 * N, dev)
+                    _hip.copy_f64(side_rep.data_ptr() + 8 * self.start, aucs_ptr, self.n_local, dev)
+                comm.all_reduce_inplace(side_rep)
+                _hip.copy_f64(slot_ptr, side_rep.data_ptr(), 2 * N, dev)
             ev = torch.cuda.Event()
             ev.record(self.side)
-            self._ev_side_done = ev
+            side["ev"] = ev
         rec["slot"] = slot
         rec["event"] = ev
         fed.round_idx += 1
