@@ -44,6 +44,21 @@ EPISODE = 20   # paper schedule: 20 rounds per run; aggregation caps reset per e
 
 
 def main(argv=None):
+    # stdout carries exactly ONE line, the JSON record: native libraries'
+    # chatter (RCCL prints a version banner to stdout when a communicator is
+    # created) is routed to stderr for the duration of the run
+    sys.stdout.flush()
+    real_stdout = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        return _main(argv, real_stdout)
+    finally:
+        sys.stdout.flush()
+        os.dup2(real_stdout, 1)
+        os.close(real_stdout)
+
+
+def _main(argv, real_stdout: int):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -186,7 +201,7 @@ def main(argv=None):
             rec["projection"] = (f"rank 0 of a {args.phantom_ranks}-rank job on ONE GPU, collectives stubbed "
                                  "(no RCCL time); value assumes every rank is as fast as this one")
         line = json.dumps(rec)
-        print(line, flush=True)
+        os.write(real_stdout, (line + "\n").encode())
         if args.out:
             with open(args.out, "w") as f:
                 f.write(line + "\n")

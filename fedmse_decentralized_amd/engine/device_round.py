@@ -155,6 +155,11 @@ class DeviceRound:
         self.rejected = torch.zeros(n, dtype=i32, device=dev)
         self.rt = _hip.runtime(dev)
         cfg = fed.cfg
+        if fed.comm.collective:
+            # persistent exchange buffers: [slots models | 1 row of vote records] per rank
+            self.xslots = fed.shard.max_local()
+            self.xsend = torch.zeros(self.xslots + 1, P_PAD, dtype=f32, device=dev)
+            self.xallg = torch.zeros(fed.comm.world_size * (self.xslots + 1), P_PAD, dtype=f32, device=dev)
         # verification: the aggregate on every hosted client's verification data (fixed mode: own V)
         if cfg.verification_method == "dev":
             vdata = [fed.dev_set for _ in fed.local]
@@ -225,7 +230,7 @@ class DeviceRound:
                 sse, _ = _hip.forward_rows(st.params, items, fed.dims, True, False)
                 _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs)
         with tel.phase("comm"):
-            if comm.world_size == 1:
+            if not comm.collective:
                 base = st.params
                 rows = np.asarray([self._loc(c) for c in selected], dtype=np.int64)
             else:
@@ -242,9 +247,11 @@ class DeviceRound:
                 # copies, which (from pageable memory) would synchronise the
                 # host with the training kernel every round.  Rows past a
                 # rank's selection are never read, so `send` needs no fill.
-                slots = max(len(v) for v in per_rank.values())
+                # The exchange buffers are persistent (a fixed slot count, the
+                # largest shard): no allocation or allocator event per round.
+                slots = self.xslots
                 mine = per_rank.get(comm.rank, [])
-                send = torch.empty(slots + 1, P_PAD, dtype=torch.float32, device=dev)
+                send, allg = self.xsend, self.xallg
                 if mine:
                     loc_ptr, cid_ptr = self.rt.desc.put(np.asarray([self._loc(c) for c in mine], dtype=np.int32),
                                                         np.asarray(mine, dtype=np.int32))
@@ -258,7 +265,7 @@ class DeviceRound:
                         n = len(mine)
                         send[n:slots].copy_(send[:1].expand(slots - n, P_PAD))
                         send[slots, 8 * n:8 * slots].copy_(send[slots, :8].repeat(slots - n))
-                allg = comm.all_gather(send).reshape(-1, P_PAD)          # [world * (slots+1), P]
+                comm.all_gather_into(allg, send)          # [world * (slots+1), P]
                 owners = [fed.shard.owner(c) for c in selected]
                 # record of client c: tail row of its owner, entry j (8-float units)
                 src = np.asarray([((o * (slots + 1) + slots) * P_PAD) // 8 + per_rank[o].index(c)
@@ -268,7 +275,6 @@ class DeviceRound:
                 base = allg
                 rows = np.asarray([o * (slots + 1) + per_rank[o].index(c) for o, c in zip(owners, selected)],
                                   dtype=np.int64)
-                rec["_keep"] = (allg, send)
         with tel.phase("aggregate"):
             noise = np.asarray(fed.noise.rand_n(k * (k - 1)), dtype=np.float64)
             sel_ptr, noise_ptr, rows_ptr = self.rt.desc.put(np.asarray(selected, dtype=np.int32),
@@ -339,7 +345,7 @@ class DeviceRound:
                 rec["snap_slot"] = si
             eng.evaluate_launch(fed.model_type, params=eval_params)
             aucs_ptr = eng._plan(fed.model_type, eval_params)["aucs_buf"].dev_ptr
-            if comm.world_size == 1:
+            if not comm.collective:
                 _hip.copy2_f64(slot_ptr, aucs_ptr, N, slot_ptr + 8 * N, side_rep.data_ptr() + 8 * N, N, dev)
             else:
                 # [AUCs | rejected counts]: one RCCL all-reduce, off the main stream

@@ -278,7 +278,7 @@ class Federation:
         single aggregator sink.
         """
         st = self.engine.store
-        if self.comm.world_size == 1:
+        if not self.comm.collective:
             rows = [self._loc(c) for c in sources]
             if rows == list(range(rows[0], rows[0] + len(rows))) if rows else False:
                 return st.params[rows[0]:rows[0] + len(rows)]

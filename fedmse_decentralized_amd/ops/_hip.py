@@ -159,7 +159,21 @@ class Runtime:
 
     def __init__(self, device: torch.device):
         self.device = device
-        self.stream = torch.cuda.current_stream(device).cuda_stream
+        cur = torch.cuda.current_stream(device)
+        self.torch_stream = None
+        if cur.cuda_stream == 0 and os.environ.get("FEDMX_NULL_STREAM", "0") != "1":
+            # Never work on the legacy null stream: it implicitly serialises
+            # with every blocking stream, and RCCL's bookkeeping on it made each
+            # round's training wait for the previous round's side-stream
+            # evaluation (+125 us per round with a one-rank RCCL group).  One
+            # non-blocking stream becomes torch's current stream of this thread,
+            # so torch ops, our launches and the collectives share one order.
+            s = torch.cuda.Stream(device=device)
+            s.wait_stream(cur)
+            torch.cuda.set_stream(s)
+            self.torch_stream = s
+            cur = s
+        self.stream = cur.cuda_stream
         self.desc = _hiprt.DescRing(4 << 20, self.stream)
         self.out = _hiprt.OutRing(4 << 20, self.stream)
 

@@ -24,6 +24,7 @@ Backends:
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import Any, List, Optional
 
@@ -35,10 +36,20 @@ class Comm:
     world_size: int = 1
     device: torch.device = torch.device("cpu")
     phantom: bool = False   # PhantomComm: collectives stubbed (single-GPU projection)
+    force_collectives: bool = False
 
     @property
     def is_root(self) -> bool:
         return self.rank == 0
+
+    @property
+    def collective(self) -> bool:
+        """Take the multi-rank code path (pack, collective, unpack).  True for
+        world size > 1, and for a world-size-1 torch.distributed group created
+        with ``FEDMX_FORCE_COLLECTIVES=1``: a one-GPU box then runs the real
+        RCCL calls and stream ordering of the multi-GPU path (RCCL refuses two
+        ranks on one GPU, so this is the only RCCL coverage one GPU allows)."""
+        return self.world_size > 1 or self.force_collectives
 
     def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
         raise NotImplementedError
@@ -49,6 +60,11 @@ class Comm:
 
     def broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
         raise NotImplementedError
+
+    def all_gather_into(self, out: torch.Tensor, t: torch.Tensor) -> None:
+        """All-gather into a caller-owned buffer of ``world * t.shape[0]`` rows
+        (persistent exchange buffers: no allocation per round)."""
+        out.copy_(self.all_gather(t).reshape(out.shape))
 
     def barrier(self) -> None:
         pass
@@ -88,6 +104,9 @@ class LoopbackComm(Comm):
     def all_gather(self, t):
         return t[None] if not isinstance(t, torch.Tensor) else t.unsqueeze(0)
 
+    def all_gather_into(self, out, t):
+        out.copy_(t.reshape(out.shape))
+
     def broadcast(self, t, src):
         return t
 
@@ -124,6 +143,9 @@ class PhantomComm(Comm):
     def all_gather(self, t):
         x = t if isinstance(t, torch.Tensor) else torch.as_tensor(t)
         return x.unsqueeze(0).expand((self.world_size,) + tuple(x.shape)).contiguous()
+
+    def all_gather_into(self, out, t):
+        out.view((self.world_size,) + tuple(t.shape)).copy_(t.unsqueeze(0).expand((self.world_size,) + tuple(t.shape)))
 
     def broadcast(self, t, src):
         return t
@@ -199,6 +221,7 @@ class TorchDistComm(Comm):
         self.rank = dist.get_rank()
         self.world_size = dist.get_world_size()
         self.backend = dist.get_backend()
+        self.force_collectives = os.environ.get("FEDMX_FORCE_COLLECTIVES", "0") == "1"
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
         self.device = torch.device(device)
@@ -219,6 +242,12 @@ class TorchDistComm(Comm):
         out = torch.empty((self.world_size * flat.shape[0],) + tuple(flat.shape[1:]), dtype=x.dtype, device=x.device)
         self.dist.all_gather_into_tensor(out, flat)
         return out.view((self.world_size,) + tuple(x.shape)).to(t.device)
+
+    def all_gather_into(self, out, t):
+        if out.device == self.device and t.device == self.device:
+            self.dist.all_gather_into_tensor(out, t)
+        else:
+            out.copy_(self.all_gather(t).reshape(out.shape))
 
     def broadcast(self, t, src):
         x = self._to(t).clone()

@@ -25,7 +25,10 @@ def init_comm(backend: Optional[str] = None, device: Optional[str] = None, timeo
     world = env_world()
     if device is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
-    if world <= 1:
+    # FEDMX_FORCE_COLLECTIVES=1 with world size 1: a real (one-rank) process
+    # group, so the multi-rank path runs its RCCL calls on a one-GPU box
+    forced = os.environ.get("FEDMX_FORCE_COLLECTIVES", "0") == "1"
+    if world <= 1 and not forced:
         dev = torch.device("cuda", 0) if device == "cuda" else torch.device("cpu")
         if dev.type == "cuda":
             torch.cuda.set_device(dev)
@@ -35,6 +38,10 @@ def init_comm(backend: Optional[str] = None, device: Optional[str] = None, timeo
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # the exchange buffers are persistent; without this, ProcessGroupNCCL's
+    # recordStream on every collective's tensors leaves events that the caching
+    # allocator then polls on each later allocation of the round loop
+    os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
     if backend is None:
         # FEDMX_DIST_BACKEND=gloo: multi-rank rehearsal on one GPU (RCCL needs distinct GPUs)
         backend = os.environ.get("FEDMX_DIST_BACKEND") or ("nccl" if device == "cuda" else "gloo")

@@ -163,3 +163,34 @@ def test_bench_phantom_ranks_projection(tmp_path):
     rec = json.loads(out.read_text())
     assert rec["config"]["clients"] == 40 and rec["config"]["device_protocol"]
     assert "projection" in rec and rec["value"] > 0
+
+
+def test_rccl_one_rank_forced_collectives_match_loopback(tmp_path):
+    """The multi-GPU code path with real RCCL on a one-GPU box: a one-rank
+    nccl (= RCCL) process group with FEDMX_FORCE_COLLECTIVES=1 packs, all-gathers
+    and all-reduces every round exactly as a rank of the N-GPU job does; its
+    results are bit-identical to the loopback (no-collective) run."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def run(extra_env, name):
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", **extra_env)
+        out = tmp_path / f"{name}.json"
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "6", "--warmup", "2",
+                            "--no-artifacts", "--out", str(out)], env=env, cwd=root, capture_output=True,
+                           text=True, timeout=150)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return json.loads(out.read_text())
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    base = run({}, "loopback")
+    forced = run({"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                  "MASTER_PORT": str(port), "FEDMX_FORCE_COLLECTIVES": "1"}, "rccl1")
+    assert forced["config"]["device_protocol"] and base["config"]["device_protocol"]
+    assert forced["detection_auc_mean"] == base["detection_auc_mean"]
+    assert forced["detection_auc_min"] == base["detection_auc_min"]

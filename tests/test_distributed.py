@@ -146,3 +146,28 @@ def test_phantom_comm_semantics():
     c.all_reduce_inplace(t)
     assert torch.equal(t, x)
     assert c.all_gather_object("h") == ["h"] * 8
+
+
+def test_forced_collectives_one_rank_gloo_matches_loopback(tmp_path):
+    """FEDMX_FORCE_COLLECTIVES=1 on a one-rank gloo group takes the multi-rank
+    host path (pack, all-gather, all-reduce) with results identical to the
+    loopback run (the CPU twin of the one-rank RCCL GPU test)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def run(extra_env, name):
+        env = dict(os.environ, **extra_env)
+        out = tmp_path / f"{name}.json"
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "2", "--warmup", "1",
+                            "--backend", "torch", "--epochs", "1", "--no-artifacts", "--out", str(out)],
+                           env=env, cwd=root, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return json.loads(out.read_text())
+
+    base = run({}, "loopback")
+    forced = run({"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                  "MASTER_PORT": str(_free_port()), "FEDMX_FORCE_COLLECTIVES": "1"}, "gloo1")
+    assert forced["detection_auc_mean"] == base["detection_auc_mean"]
+    assert forced["detection_auc_min"] == base["detection_auc_min"]
