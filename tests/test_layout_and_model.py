@@ -86,3 +86,27 @@ def test_fwd_rows_per_block_fills_the_chip_without_a_straggler_wave():
         blocks = sum(-(-n // rpb) for n in per_item)
         if rpb > 64:
             assert blocks <= FWD_BLOCK_SLOTS
+
+
+def test_xcd_order_groups_shared_rows_on_one_xcd():
+    """Items scoring several models on the same rows (the FedMSE dev set) are
+    laid out so every model's block of a row range shares blockIdx % 8 (one
+    XCD L2); every real block appears exactly once, fillers are -1."""
+    from fedmse_decentralized_amd.ops._hip import XCDS, _xcd_order
+
+    nrows = np.array([169, 169, 6650, 6650, 6650, 300], dtype=np.int64)
+    x = np.array([10, 10, 99, 99, 99, 7], dtype=np.int64)       # items 2-4 share their rows
+    rpb = 64
+    nblk = (nrows + rpb - 1) // rpb
+    first = np.cumsum(nblk) - nblk
+    order = _xcd_order(x, nrows, nblk)
+    real = order[order >= 0]
+    assert sorted(real.tolist()) == list(range(int(nblk.sum())))
+    pos = {int(b): p for p, b in enumerate(order) if b >= 0}
+    for r in range(int(nblk[2])):
+        lanes = {pos[int(first[it]) + r] % XCDS for it in (2, 3, 4)}
+        assert lanes == {r % XCDS}
+    assert len(order) - len(real) < XCDS * 3          # few fillers
+    # nothing shared (or too short to matter): plain item order
+    assert _xcd_order(np.array([1, 2]), np.array([640, 640]), np.array([10, 10])) is None
+    assert _xcd_order(np.array([1, 1]), np.array([64, 64]), np.array([1, 1])) is None
