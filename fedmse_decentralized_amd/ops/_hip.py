@@ -172,6 +172,7 @@ class Runtime:
             s.wait_stream(cur)
             torch.cuda.set_stream(s)
             self.torch_stream = s
+            _tls.rt_thread = self
             cur = s
         self.stream = cur.cuda_stream
         self.desc = _hiprt.DescRing(4 << 20, self.stream)
@@ -184,15 +185,22 @@ class Runtime:
 _runtimes: Dict[Tuple[str, int], Runtime] = {}
 
 
+_tls = threading.local()
+
+
 def runtime(device: torch.device) -> Runtime:
     key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
     r = _runtimes.get(key)
     if r is None:
         r = _runtimes[key] = Runtime(torch.device("cuda", key[1]))
+    if r.torch_stream is not None and getattr(_tls, "rt_thread", None) is not r:
+        # torch's current stream is per thread: a thread that first touches the
+        # runtime while still on the null stream joins the runtime's stream
+        if torch.cuda.current_stream(r.device).cuda_stream == 0:
+            r.torch_stream.wait_stream(torch.cuda.current_stream(r.device))
+            torch.cuda.set_stream(r.torch_stream)
+        _tls.rt_thread = r
     return r
-
-
-_tls = threading.local()
 
 
 def _stream(device: torch.device) -> int:
