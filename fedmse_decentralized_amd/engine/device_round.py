@@ -221,11 +221,19 @@ class DeviceRound:
                 torch.cuda.current_stream(dev).wait_event(ev_std)
                 need_dev = self.rule == 1
                 items = [(r, vs) for r in local_rows]
-                outs = [self.vec[c].data_ptr() for c in local_sel]
+                # each client's record [vote score, -, dev MSE, dev MSE] (4 doubles):
+                # with collectives straight into the exchange buffer's tail row
+                # (slot j = j-th local selection, the pack order), else into vec
+                if comm.collective:
+                    tail = self.xsend[self.xslots].data_ptr()
+                    recp = [tail + 32 * j for j in range(len(local_sel))]
+                else:
+                    recp = [self.vec[c].data_ptr() for c in local_sel]
+                outs = list(recp)
                 batch = [cfg.vote_batch_size] * len(local_rows)
                 if need_dev:
                     items += [(r, fed.dev_set) for r in local_rows]
-                    outs += [self.vec[c].data_ptr() + 16 for c in local_sel]
+                    outs += [p + 16 for p in recp]
                     batch += [0] * len(local_rows)
                 sse, _ = _hip.forward_rows(st.params, items, fed.dims, True, False)
                 _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs)
@@ -253,12 +261,10 @@ class DeviceRound:
                 mine = per_rank.get(comm.rank, [])
                 send, allg = self.xsend, self.xallg
                 if mine:
-                    loc_ptr, cid_ptr = self.rt.desc.put(np.asarray([self._loc(c) for c in mine], dtype=np.int32),
-                                                        np.asarray(mine, dtype=np.int32))
+                    # (the vote records are already in the tail row: score_reduce wrote them there)
+                    (loc_ptr,) = self.rt.desc.put(np.asarray([self._loc(c) for c in mine], dtype=np.int32))
                     _hip.copy_rows(send.data_ptr(), P_PAD, 0, st.params.data_ptr(), P_PAD, loc_ptr, len(mine),
                                    P_PAD, dev)
-                    # vote records: 4 doubles = 8 floats per client, packed into the tail row
-                    _hip.copy_rows(send[slots].data_ptr(), 8, 0, self.vec.data_ptr(), 8, cid_ptr, len(mine), 8, dev)
                     if comm.phantom and len(mine) < slots:
                         # single-GPU projection (PhantomComm): other ranks' rows are
                         # copies of this rank's, so the spare slots must hold real models
@@ -267,24 +273,29 @@ class DeviceRound:
                         send[slots, 8 * n:8 * slots].copy_(send[slots, :8].repeat(slots - n))
                 comm.all_gather_into(allg, send)          # [world * (slots+1), P]
                 owners = [fed.shard.owner(c) for c in selected]
-                # record of client c: tail row of its owner, entry j (8-float units)
-                src = np.asarray([((o * (slots + 1) + slots) * P_PAD) // 8 + per_rank[o].index(c)
-                                  for o, c in zip(owners, selected)], dtype=np.int32)
-                src_ptr, dst_ptr = self.rt.desc.put(src, np.asarray(selected, dtype=np.int32))
-                _hip.copy_rows(self.vec.data_ptr(), 8, dst_ptr, allg.data_ptr(), 8, src_ptr, k, 8, dev)
+                # record of client c: tail row of its owner, entry j (4-double units);
+                # the election reads the records in place through this table
+                rec_idx = np.asarray([((o * (slots + 1) + slots) * P_PAD) // 8 + per_rank[o].index(c)
+                                      for o, c in zip(owners, selected)], dtype=np.int32)
                 base = allg
                 rows = np.asarray([o * (slots + 1) + per_rank[o].index(c) for o, c in zip(owners, selected)],
                                   dtype=np.int64)
         with tel.phase("aggregate"):
             noise = np.asarray(fed.noise.rand_n(k * (k - 1)), dtype=np.float64)
-            sel_ptr, noise_ptr, rows_ptr = self.rt.desc.put(np.asarray(selected, dtype=np.int32),
-                                                            noise if noise.size else np.zeros(1), rows)
+            if comm.collective:
+                sel_ptr, noise_ptr, rows_ptr, rec_ptr = self.rt.desc.put(
+                    np.asarray(selected, dtype=np.int32), noise if noise.size else np.zeros(1), rows, rec_idx)
+                vec_ptr = base.data_ptr()
+            else:
+                sel_ptr, noise_ptr, rows_ptr = self.rt.desc.put(np.asarray(selected, dtype=np.int32),
+                                                                noise if noise.size else np.zeros(1), rows)
+                rec_ptr, vec_ptr = 0, self.vec.data_ptr()
             rep_ptr, rep_view = self.rt.out.take(np.int32, 2)
             rep_view[:] = -2
-            a = _hip.ElectArgs(sel=sel_ptr, vec=self.vec.data_ptr(), noise=noise_ptr,
+            a = _hip.ElectArgs(sel=sel_ptr, vec=vec_ptr, noise=noise_ptr,
                                agg_counts=self.agg_counts.data_ptr(), weights=self.weights.data_ptr(),
                                state=self.state.data_ptr(), report=rep_ptr, k=k, cap=cfg.max_aggregation,
-                               rule=self.rule, pad=0)
+                               rule=self.rule, pad=0, rec=rec_ptr)
             w = _hip.WsumArgs(base=base.data_ptr(), rows=rows_ptr, weights=self.weights.data_ptr(),
                               state=self.state.data_ptr(), out=self.agg.data_ptr(), k=k, P=P_PAD)
             _hip.elect_wsum(a, w, dev)

@@ -39,8 +39,10 @@ struct ElectArgs {
   int32_t* report;         // [2] out (mapped host memory): aggregator, voter
   int32_t k, cap, rule;    // rule 0: mean (avg / fedprox), 1: 1/MSE (mse_avg)
   int32_t pad;
+  const int32_t* rec;      // [k] record index (4-double units into vec) of each selection, or
+                           // null: the client id (multi-rank: records read in place from the exchange buffer)
 };
-static_assert(sizeof(ElectArgs) == 72, "ElectArgs layout is shared with Python");
+static_assert(sizeof(ElectArgs) == 80, "ElectArgs layout is shared with Python");
 
 struct WsumArgs {
   const float* base;       // row-major [*, P]
@@ -81,8 +83,9 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
       double vs = 0.0, mse = 1.0;
       if (lane < k) {
         c = E.sel[lane];
-        vs = E.vec[(size_t)c * 4];
-        mse = E.vec[(size_t)c * 4 + 3];
+        const int ri = E.rec != nullptr ? E.rec[lane] : c;
+        vs = E.vec[(size_t)ri * 4];
+        mse = E.vec[(size_t)ri * 4 + 3];
         cnt = E.agg_counts[c];
       }
       int agg = -1, voter = -1;
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
         const int c = E.sel[ci];
         if (c == v) continue;
         const double f = 1.0 + (u[j++] - 0.5) * 0.0002;
-        const double sc = E.vec[(size_t)c * 4] * f;
+        const double sc = E.vec[(size_t)(E.rec != nullptr ? E.rec[ci] : c) * 4] * f;
         if (E.agg_counts[c] < E.cap && (best < 0 || sc < best_s)) {
           best = c;
           best_s = sc;
@@ -160,8 +163,9 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
     if (agg >= 0) {
       if (E.rule == 1) {
         double tot = 0.0;
-        for (int j = 0; j < E.k; ++j) tot += 1.0 / E.vec[(size_t)E.sel[j] * 4 + 3];
-        for (int j = 0; j < E.k; ++j) s_w[j] = (float)((1.0 / E.vec[(size_t)E.sel[j] * 4 + 3]) / tot);
+        for (int j = 0; j < E.k; ++j) tot += 1.0 / E.vec[(size_t)(E.rec != nullptr ? E.rec[j] : E.sel[j]) * 4 + 3];
+        for (int j = 0; j < E.k; ++j)
+          s_w[j] = (float)((1.0 / E.vec[(size_t)(E.rec != nullptr ? E.rec[j] : E.sel[j]) * 4 + 3]) / tot);
       } else {
         const float w = (float)(1.0 / (double)E.k);
         for (int j = 0; j < E.k; ++j) s_w[j] = w;
