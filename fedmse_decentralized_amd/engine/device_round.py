@@ -156,7 +156,7 @@ class DeviceRound:
         self.rt = _hip.runtime(dev)
         cfg = fed.cfg
         if fed.comm.collective:
-            # persistent exchange buffers: [slots models | 1 row of vote records] per rank
+            # persistent exchange buffers: [1 row of vote records | up to xslots models] per rank
             self.xslots = fed.shard.max_local()
             self.xsend = torch.zeros(self.xslots + 1, P_PAD, dtype=f32, device=dev)
             self.xallg = torch.zeros(fed.comm.world_size * (self.xslots + 1), P_PAD, dtype=f32, device=dev)
@@ -225,8 +225,8 @@ class DeviceRound:
                 # with collectives straight into the exchange buffer's tail row
                 # (slot j = j-th local selection, the pack order), else into vec
                 if comm.collective:
-                    tail = self.xsend[self.xslots].data_ptr()
-                    recp = [tail + 32 * j for j in range(len(local_sel))]
+                    head = self.xsend[0].data_ptr()
+                    recp = [head + 32 * j for j in range(len(local_sel))]
                 else:
                     recp = [self.vec[c].data_ptr() for c in local_sel]
                 outs = list(recp)
@@ -255,30 +255,33 @@ class DeviceRound:
                 # copies, which (from pageable memory) would synchronise the
                 # host with the training kernel every round.  Rows past a
                 # rank's selection are never read, so `send` needs no fill.
-                # The exchange buffers are persistent (a fixed slot count, the
-                # largest shard): no allocation or allocator event per round.
-                slots = self.xslots
+                # The exchange buffers are persistent (sized for the largest
+                # shard): no allocation or allocator event per round; each
+                # round exchanges only the prefix [records row | slots model
+                # rows] that its largest per-rank selection needs.
+                slots = max(len(v) for v in per_rank.values())
                 mine = per_rank.get(comm.rank, [])
-                send, allg = self.xsend, self.xallg
+                send = self.xsend[:slots + 1]
+                allg = self.xallg[:comm.world_size * (slots + 1)]
                 if mine:
-                    # (the vote records are already in the tail row: score_reduce wrote them there)
+                    # (the vote records are already in row 0: score_reduce wrote them there)
                     (loc_ptr,) = self.rt.desc.put(np.asarray([self._loc(c) for c in mine], dtype=np.int32))
-                    _hip.copy_rows(send.data_ptr(), P_PAD, 0, st.params.data_ptr(), P_PAD, loc_ptr, len(mine),
+                    _hip.copy_rows(send[1].data_ptr(), P_PAD, 0, st.params.data_ptr(), P_PAD, loc_ptr, len(mine),
                                    P_PAD, dev)
                     if comm.phantom and len(mine) < slots:
                         # single-GPU projection (PhantomComm): other ranks' rows are
                         # copies of this rank's, so the spare slots must hold real models
                         n = len(mine)
-                        send[n:slots].copy_(send[:1].expand(slots - n, P_PAD))
-                        send[slots, 8 * n:8 * slots].copy_(send[slots, :8].repeat(slots - n))
+                        send[1 + n:1 + slots].copy_(send[1:2].expand(slots - n, P_PAD))
+                        send[0, 8 * n:8 * slots].copy_(send[0, :8].repeat(slots - n))
                 comm.all_gather_into(allg, send)          # [world * (slots+1), P]
                 owners = [fed.shard.owner(c) for c in selected]
-                # record of client c: tail row of its owner, entry j (4-double units);
-                # the election reads the records in place through this table
-                rec_idx = np.asarray([((o * (slots + 1) + slots) * P_PAD) // 8 + per_rank[o].index(c)
+                # record of client c: row 0 of its owner's block, entry j (4-double
+                # units); the election reads the records in place through this table
+                rec_idx = np.asarray([(o * (slots + 1) * P_PAD) // 8 + per_rank[o].index(c)
                                       for o, c in zip(owners, selected)], dtype=np.int32)
                 base = allg
-                rows = np.asarray([o * (slots + 1) + per_rank[o].index(c) for o, c in zip(owners, selected)],
+                rows = np.asarray([o * (slots + 1) + 1 + per_rank[o].index(c) for o, c in zip(owners, selected)],
                                   dtype=np.int64)
         with tel.phase("aggregate"):
             noise = np.asarray(fed.noise.rand_n(k * (k - 1)), dtype=np.float64)
