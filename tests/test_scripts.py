@@ -38,3 +38,26 @@ def test_prof_summary_on_synthetic_db(tmp_path):
     c.commit()
     s = prof_summary.summarize(str(db), "t")
     assert "fedmx::train_kernel<false>" in s and "one round timeline" in s
+
+
+def test_bench_stdout_is_one_json_line():
+    """The driver contract: `python bench.py ...` prints exactly one JSON line
+    on stdout with the BASELINE metric and the required fields (CPU engine,
+    one short round)."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--backend", "torch", "--steps", "1",
+                        "--warmup", "0", "--epochs", "1", "--no-artifacts"], cwd=root, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in rec, k
+    assert rec["n_gpus"] == 1 and rec["steps"] == 1 and rec["warmup"] == 0 and rec["scaling"] == "weak"
+    assert rec["higher_is_better"] is True and rec["value"] > 0
+    for k in ("model", "global_batch", "seq_len", "parallelism"):
+        assert k in rec["config"], k
