@@ -22,6 +22,7 @@ __global__ __launch_bounds__(256) void fwd_rows_kernel(const FwdDesc* __restrict
   __shared__ __attribute__((aligned(16))) float sW4[DP * S_W4];
 
   const FwdDesc d = descs[blockIdx.x];
+  if (d.nrows <= 0) return;   // alignment filler of an XCD-grouped descriptor list (whole block)
   stage_params(d.params, sW1, sW2, sW3, sW4);
   __syncthreads();
   fwd_rows_block(d, sW1, sW2, sW3, sW4, threadIdx.x >> 6, 4, d.sse);
