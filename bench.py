@@ -135,6 +135,7 @@ def _main(argv, real_stdout: int):
 
         prof = cProfile.Profile()
         prof.enable()
+    fed.tel.reset_totals()   # phase totals cover the timed rounds only
     t0 = time.perf_counter()
     w_busy0 = fed.writer.busy_s
     last = None
@@ -160,23 +161,40 @@ def _main(argv, real_stdout: int):
     allt = comm.all_gather(t)
     dt = float(allt.max())
     fed_rps = args.steps / dt
-    value = fed_rps * (fed.N / 10.0)
-    auc = float(np.mean(last.metrics)) if last is not None else float("nan")
+    phantom = args.phantom_ranks > 1
+    # whole-job value: with the default 10 clients per GPU the federation has
+    # 10*N clients and the job does N 10-client federations' worth of work
+    # per round; for a fixed federation size (--clients) the round rate itself
+    world_for_value = args.phantom_ranks if phantom else n_gpus
+    per_gpu_default = args.clients is None and args.clients_per_gpu == 10
+    value = fed_rps * world_for_value if per_gpu_default else fed_rps
+    if last is not None:
+        # a phantom rank only ever evaluates its own clients (the AUC
+        # all-reduce is stubbed): report those, not the zero-filled others
+        m = np.asarray(last.metrics, dtype=np.float64)
+        if phantom and fed.local:
+            m = m[fed.local[0]:fed.local[-1] + 1]
+        auc, auc_min = float(np.mean(m)), float(np.min(m))
+    else:
+        auc = auc_min = float("nan")
     if comm.is_root:
+        unit = ("rounds/s (10-client-federation equivalents, whole job)" if per_gpu_default
+                else "federation rounds/s")
         rec = {
             "metric": METRIC,
-            "value": round(value, 4),
-            "unit": "rounds/s (10-client-federation equivalents, whole job)",
-            "n_gpus": n_gpus,
+            "value": None if phantom else round(value, 4),
+            "unit": unit,
+            "n_gpus": 1 if phantom else n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * dt / args.steps, 4),
             "higher_is_better": True,
             "scaling": "strong" if args.clients else "weak",
-            "vs_baseline": round(value / BASELINE_ROUNDS_PER_SEC, 2),
+            "vs_baseline": None if phantom else round(value / BASELINE_ROUNDS_PER_SEC, 2),
             "dtype": "fp32",
             "data": (f"synthetic ({'N-BaIoT' if args.data_kind == 'nbaiot' else 'Kitsune'}-shaped, 115 features, "
-                     f"{'non-IID' if args.non_iid else 'IID'} client mixtures, IID-10 client sizes); "
+                     f"{'non-IID (Dirichlet)' if args.non_iid else 'IID'} client mixtures, "
+                     f"{'IID-10 client sizes' if not args.non_iid else 'Dirichlet client sizes'}); "
                      "random-init weights"),
             "config": {
                 "model": f"SAE 115-27-7-27-115 ({args.model_type}, {args.update_type}), "
@@ -193,13 +211,18 @@ def _main(argv, real_stdout: int):
             },
             "federation_rounds_per_sec": round(fed_rps, 4),
             "detection_auc_mean": round(auc, 6),
-            "detection_auc_min": round(float(np.min(last.metrics)), 6) if last is not None else None,
+            "detection_auc_min": round(auc_min, 6),
             "phase_ms_total": {k: round(v, 3) for k, v in fed.tel.summary().items()},
             "writer_busy_ms_per_round": round(1e3 * (fed.writer.busy_s - w_busy0) / args.steps, 4),
         }
-        if args.phantom_ranks > 1:
+        if phantom:
+            # a one-GPU projection, not a multi-GPU measurement: n_gpus stays 1
+            # and the whole-job figure goes to projected_value
+            rec["projected_ranks"] = args.phantom_ranks
+            rec["projected_value"] = round(value, 4)
+            rec["detection_auc_scope"] = "rank-0 clients only"
             rec["projection"] = (f"rank 0 of a {args.phantom_ranks}-rank job on ONE GPU, collectives stubbed "
-                                 "(no RCCL time); value assumes every rank is as fast as this one")
+                                 "(no RCCL time); projected_value assumes every rank is as fast as this one")
         line = json.dumps(rec)
         os.write(real_stdout, (line + "\n").encode())
         if args.out:

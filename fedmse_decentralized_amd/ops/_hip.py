@@ -272,7 +272,7 @@ def build_fwd_desc(param_ptrs: np.ndarray, x_ptrs: np.ndarray, nrows: np.ndarray
     if order is not None:
         pad = order < 0
         desc = desc[np.where(pad, 0, order)]
-        desc["nrows"][pad] = 0   # alignment filler: stages params, no rows
+        desc["nrows"][pad] = 0   # alignment filler: no rows, the block exits immediately
     return desc
 
 

@@ -78,3 +78,9 @@ class Telemetry:
 
     def summary(self) -> Dict[str, float]:
         return {k: v * 1e3 for k, v in self.total.items()}
+
+    def reset_totals(self) -> None:
+        """Start the accumulated per-phase totals afresh (e.g. after warm-up
+        rounds, so a benchmark's totals cover only its timed rounds)."""
+        self.total = defaultdict(float)
+        self.counts = defaultdict(int)

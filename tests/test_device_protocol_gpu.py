@@ -162,7 +162,11 @@ def test_bench_phantom_ranks_projection(tmp_path):
                        "--out", str(out)]) == 0
     rec = json.loads(out.read_text())
     assert rec["config"]["clients"] == 40 and rec["config"]["device_protocol"]
-    assert "projection" in rec and rec["value"] > 0
+    # a projection is never recorded as a multi-GPU measurement
+    assert "projection" in rec and rec["value"] is None and rec["n_gpus"] == 1
+    assert rec["projected_ranks"] == 4 and rec["projected_value"] > 0
+    # only rank 0's own clients are evaluated: their AUCs, not zero-filled ones
+    assert rec["detection_auc_min"] > 0.5
 
 
 def test_rccl_one_rank_forced_collectives_match_loopback(tmp_path):
