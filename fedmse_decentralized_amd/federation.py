@@ -242,19 +242,17 @@ class Federation:
         reports.append_verification(self.cfg, self.run, rnd, vr, files=self.writer.files)
 
     def _submit_checkpoints(self, res, local_sel: Sequence[int], snap, ev) -> None:
-        dims = self.dims
-        cidx = self._canon_idx
-        for i, c in enumerate(local_sel):
-            d = self.save_dirs[c]
-            row = self._loc(c)
-            improved = res.best_epoch[i] >= 0
-            trk = list(res.tracking[i])
+        # one job per round: every trained client's model.cpt + tracking pickle
+        # rendered and written by the native batched writer (io.checkpoint)
+        dirs = [self.save_dirs[c] for c in local_sel]
+        rows = [self._loc(c) for c in local_sel]
+        improved = [bool(res.best_epoch[i] >= 0) for i in range(len(local_sel))]
+        trks = [list(res.tracking[i]) for i in range(len(local_sel))]
+        dims, cidx = self.dims, self._canon_idx
 
-            def job(d=d, row=row, improved=improved, trk=trk, files=self.writer.files):
-                if improved:
-                    ckpt.save_model_cpt_fast(d, snap[row].numpy()[cidx], dims, files=files)
-                ckpt.save_tracking(d, trk, files=files)
-            self.writer.submit(job, ev)
+        def job(files=self.writer.files):
+            ckpt.write_round_artifacts(files, dirs, snap.numpy(), rows, improved, trks, cidx, dims)
+        self.writer.submit(job, ev)
 
     def _resume_path(self, base: str) -> str:
         return base if self.comm.world_size == 1 else f"{base}.rank{self.comm.rank}"

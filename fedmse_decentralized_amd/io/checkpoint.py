@@ -111,6 +111,70 @@ def save_model_cpt_fast(save_dir: str, canonical: np.ndarray, dims: ModelDims = 
     return path
 
 
+def _template(dims: ModelDims) -> "_CptTemplate":
+    tpl = _TEMPLATES.get(dims)
+    if tpl is None:
+        tpl = _TEMPLATES[dims] = _CptTemplate(dims)
+    if not hasattr(tpl, "np_blob"):
+        tpl.np_blob = np.frombuffer(bytes(tpl.blob), dtype=np.uint8)
+        tpl.np_regions = np.ascontiguousarray(np.asarray(tpl.regions, dtype=np.int64).reshape(-1, 3))
+    return tpl
+
+
+_PATHS: Dict[str, Tuple[str, str]] = {}
+
+
+def _artifact_paths(save_dir: str) -> Tuple[str, str]:
+    p = _PATHS.get(save_dir)
+    if p is None:
+        p = _PATHS[save_dir] = (os.path.join(save_dir, "model.cpt"), os.path.join(save_dir, "training_tracking.pkl"))
+    return p
+
+
+def write_round_artifacts(files, save_dirs: Sequence[str], snap: np.ndarray, rows: Sequence[int],
+                          improved: Sequence[bool], tracking: Sequence[Sequence[Tuple[float, float]]],
+                          canon_idx: np.ndarray, dims: ModelDims = DEFAULT_DIMS, n_threads: int = 0) -> None:
+    """Every trained client's ``model.cpt`` (when its validation improved) and
+    ``training_tracking.pkl`` for one round, in ONE native call
+    (``ops/csrc/host/fedmx_artifacts.cpp``: template patch + exact protocol-4
+    pickle + pwrite into cached descriptors, on a few threads, GIL released).
+    The bytes are those of ``save_model_cpt_fast`` / ``save_tracking``; a
+    job the native path cannot render (> 1000 tracked epochs) falls back to
+    them.  ``snap`` is the padded host snapshot [rows, P_PAD] fp32."""
+    from ..ops import _host
+
+    n = len(save_dirs)
+    if n == 0:
+        return
+    tpl = _template(dims)
+    cpt_paths, trk_paths = zip(*[_artifact_paths(d) for d in save_dirs])
+    fd_cpt = np.asarray([files.open_overwrite(p, 2 * n) for p in cpt_paths], dtype=np.int32)
+    fd_trk = np.asarray([files.open_overwrite(p, 2 * n) for p in trk_paths], dtype=np.int32)
+    size_cpt = np.asarray([files.size_of(p) for p in cpt_paths], dtype=np.int64)
+    size_trk = np.asarray([files.size_of(p) for p in trk_paths], dtype=np.int64)
+    lens = np.asarray([len(t) for t in tracking], dtype=np.int32)
+    trk = np.zeros((n, max(1, int(lens.max(initial=0))), 2), dtype=np.float64)
+    for j, t in enumerate(tracking):
+        if len(t):
+            trk[j, :len(t)] = np.asarray(t, dtype=np.float64).reshape(-1, 2)
+    if n_threads <= 0:
+        n_threads = max(1, min(4, n // 8))
+    snap = np.ascontiguousarray(snap, dtype=np.float32)
+    status = _host.write_artifacts(snap, np.ascontiguousarray(canon_idx, dtype=np.int32), tpl.np_blob,
+                                   tpl.np_regions, np.asarray(rows, dtype=np.int32),
+                                   np.asarray(improved, dtype=np.int32), fd_cpt, fd_trk, size_cpt, size_trk,
+                                   trk, lens, n_threads)
+    for j in range(n):
+        files.set_size(cpt_paths[j], size_cpt[j])
+        files.set_size(trk_paths[j], size_trk[j])
+        if status[j] == -1:      # too many epochs for the native pickler
+            if improved[j]:
+                save_model_cpt_fast(save_dirs[j], snap[rows[j]][canon_idx], dims, files=files)
+            save_tracking(save_dirs[j], tracking[j], files=files)
+        elif status[j] != 0:
+            raise OSError(-int(status[j]), f"writing the artefacts of {save_dirs[j]}")
+
+
 def save_model_cpt(save_dir: str, padded_params: torch.Tensor, dims: ModelDims = DEFAULT_DIMS) -> str:
     os.makedirs(save_dir, exist_ok=True)
     flat = padded_to_canonical(padded_params.detach().float().cpu(), dims)

@@ -56,6 +56,20 @@ class ArtifactFiles:
             os.ftruncate(fd, n)
         self._size[path] = n
 
+    def open_overwrite(self, path: str, reserve: int = 0) -> int:
+        """Cached descriptor for in-place rewrites of ``path`` (for a native
+        writer); ``reserve`` keeps that many descriptors from being evicted by
+        the opens of one batch."""
+        if reserve > self.max_open - 16:
+            self.max_open = reserve + 16
+        return self._fd(path, "w")
+
+    def size_of(self, path: str) -> int:
+        return self._size.get(path, 0)
+
+    def set_size(self, path: str, n: int) -> None:
+        self._size[path] = int(n)
+
     def append(self, path: str, data: bytes) -> None:
         fd = self._fd(path, "a")
         view = memoryview(data)

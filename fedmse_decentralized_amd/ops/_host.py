@@ -27,6 +27,14 @@ def lib():
             L.fedmx_csv_parse.restype = ctypes.c_int64
             L.fedmx_roc_auc.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
             L.fedmx_roc_auc.restype = ctypes.c_double
+            L.fedmx_pickle_tracking.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64]
+            L.fedmx_pickle_tracking.restype = ctypes.c_int64
+            L.fedmx_write_artifacts.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
+                                                ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
+                                                ctypes.c_int32] + [ctypes.c_void_p] * 8 + [ctypes.c_int32,
+                                                                                          ctypes.c_void_p,
+                                                                                          ctypes.c_int32]
+            L.fedmx_write_artifacts.restype = ctypes.c_int32
             _lib = L
     return _lib
 
@@ -53,3 +61,34 @@ def roc_auc(score: np.ndarray, label: np.ndarray) -> float:
     s = np.ascontiguousarray(score, dtype=np.float64)
     y = np.ascontiguousarray(label, dtype=np.int64)
     return float(lib().fedmx_roc_auc(s.ctypes.data, y.ctypes.data, s.shape[0]))
+
+
+def pickle_tracking(tracking) -> bytes:
+    """pickle.dumps([(train, valid), ...], protocol=4), rendered natively."""
+    t = np.ascontiguousarray(np.asarray(tracking, dtype=np.float64).reshape(-1, 2))
+    cap = 16 + 20 * t.shape[0]
+    out = np.empty(cap, dtype=np.uint8)
+    n = lib().fedmx_pickle_tracking(t.ctypes.data, t.shape[0], out.ctypes.data, cap)
+    if n < 0:
+        raise ValueError("tracking too long for the native pickler")
+    return out[:n].tobytes()
+
+
+def write_artifacts(snap: np.ndarray, canon_idx: np.ndarray, tpl: np.ndarray, regions: np.ndarray,
+                    rows: np.ndarray, improved: np.ndarray, fd_cpt: np.ndarray, fd_trk: np.ndarray,
+                    size_cpt: np.ndarray, size_trk: np.ndarray, trk: np.ndarray, trk_len: np.ndarray,
+                    n_threads: int = 1) -> np.ndarray:
+    """One round's model.cpt + training_tracking.pkl files (see
+    csrc/host/fedmx_artifacts.cpp).  ``size_cpt`` / ``size_trk`` are updated in
+    place; returns the per-job status (0 = written)."""
+    n = int(rows.shape[0])
+    status = np.zeros(n, dtype=np.int32)
+    assert snap.dtype == np.float32 and snap.flags.c_contiguous and trk.dtype == np.float64
+    assert trk.shape[0] >= n and trk.shape[2] == 2 and trk.flags.c_contiguous
+    lib().fedmx_write_artifacts(
+        snap.ctypes.data, snap.shape[1], canon_idx.ctypes.data, canon_idx.shape[0],
+        tpl.ctypes.data, tpl.shape[0], regions.ctypes.data, regions.shape[0], n,
+        rows.ctypes.data, improved.ctypes.data, fd_cpt.ctypes.data, fd_trk.ctypes.data,
+        size_cpt.ctypes.data, size_trk.ctypes.data, trk.ctypes.data, trk_len.ctypes.data, trk.shape[1],
+        status.ctypes.data, n_threads)
+    return status

@@ -1,0 +1,170 @@
+// Batched per-round checkpoint artefact writer (C++17, no GPU dependency).
+//
+// Every round the reference rewrites, for each trained client, its
+// best-validation `model.cpt` (legacy torch serialisation, written by
+// `save_model`, src/Trainer/client_trainer.py:337-350) and its
+// `training_tracking.pkl` (pickle protocol 4 of [(train_loss, valid_loss)],
+// :416/:419).  In Python that is ~70-150 us of GIL-holding work per client
+// (gather of the canonical parameters, template patch, pickle, two writes),
+// which made the background writer the bound of large federations (64
+// clients: 4.8 ms of writer time per round).  Here ONE call renders and
+// writes every client of a round on a few threads, without the GIL:
+//
+//   * model.cpt: the byte template of the legacy format (produced once by
+//     torch.save itself, io/checkpoint.py:_CptTemplate) with the canonical
+//     parameters gathered from the padded host snapshot row and patched into
+//     the storage regions; written with one pwrite at offset 0 into an
+//     already-open descriptor.
+//   * training_tracking.pkl: the exact bytes pickle.dumps(list_of_tuples,
+//     protocol=4) produces (PROTO 4, FRAME when the body is >= 4 bytes,
+//     EMPTY_LIST MEMOIZE, MARK ... APPENDS (or APPEND for one element),
+//     BINFLOAT x2 TUPLE2 MEMOIZE per epoch, STOP); tested byte-for-byte
+//     against Python's pickle (tests/test_files.py).
+//
+// A file shrinks (ftruncate) only when its new content is shorter than what
+// it held, so a steady-state rewrite is a single pwrite.
+//
+// C ABI; loaded with ctypes from fedmse_decentralized_amd/ops/_host.py.
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <unistd.h>
+#include <vector>
+
+namespace {
+
+inline void put_be_f64(std::vector<uint8_t>& b, double v) {
+  uint64_t u;
+  std::memcpy(&u, &v, 8);
+  for (int i = 7; i >= 0; --i) b.push_back(static_cast<uint8_t>(u >> (8 * i)));
+}
+
+inline void put_le_u64(uint8_t* p, uint64_t v) {
+  for (int i = 0; i < 8; ++i) p[i] = static_cast<uint8_t>(v >> (8 * i));
+}
+
+// pickle.dumps([(a0, b0), (a1, b1), ...], protocol=4) for n <= 1000 (one
+// APPENDS batch, one frame).  Returns false for larger n (caller falls back).
+bool pickle_tracking(const double* t, int n, std::vector<uint8_t>& out) {
+  if (n < 0 || n > 1000) return false;
+  std::vector<uint8_t> body;
+  body.reserve(4 + 20 * static_cast<size_t>(n));
+  body.push_back(']');   // EMPTY_LIST
+  body.push_back(0x94);  // MEMOIZE
+  if (n >= 2) body.push_back('(');  // MARK
+  for (int i = 0; i < n; ++i) {
+    body.push_back('G');
+    put_be_f64(body, t[2 * i]);
+    body.push_back('G');
+    put_be_f64(body, t[2 * i + 1]);
+    body.push_back(0x86);  // TUPLE2
+    body.push_back(0x94);  // MEMOIZE
+  }
+  if (n >= 2) body.push_back('e');       // APPENDS
+  else if (n == 1) body.push_back('a');  // APPEND
+  body.push_back('.');                   // STOP
+  out.clear();
+  out.push_back(0x80);  // PROTO
+  out.push_back(4);
+  if (body.size() >= 4) {   // pickle's framer skips frames shorter than 4 bytes
+    uint8_t hdr[9];
+    hdr[0] = 0x95;  // FRAME
+    put_le_u64(hdr + 1, body.size());
+    out.insert(out.end(), hdr, hdr + 9);
+  }
+  out.insert(out.end(), body.begin(), body.end());
+  return true;
+}
+
+int write_all(int fd, const uint8_t* p, size_t n, int64_t* size_io) {
+  size_t off = 0;
+  while (off < n) {
+    const ssize_t w = pwrite(fd, p + off, n - off, static_cast<off_t>(off));
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return -errno;
+    }
+    off += static_cast<size_t>(w);
+  }
+  if (*size_io > static_cast<int64_t>(n)) {
+    if (ftruncate(fd, static_cast<off_t>(n)) != 0) return -errno;
+  }
+  *size_io = static_cast<int64_t>(n);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Bytes of pickle.dumps(tracking, protocol=4) into out (capacity cap);
+// returns the length, -1 if unsupported, -2 if cap is too small.
+int64_t fedmx_pickle_tracking(const double* t, int32_t n, uint8_t* out, int64_t cap) {
+  std::vector<uint8_t> b;
+  if (!pickle_tracking(t, n, b)) return -1;
+  if (static_cast<int64_t>(b.size()) > cap) return -2;
+  std::memcpy(out, b.data(), b.size());
+  return static_cast<int64_t>(b.size());
+}
+
+// One round's artefacts for n_jobs clients.
+//   snap [*, snap_stride] f32 host snapshot; canon_idx[n_canon] gathers the
+//   canonical parameter vector out of a padded row; tpl/regions: the legacy
+//   model.cpt template and its (byte pos, count, canonical offset) triples.
+//   Job j: snapshot row rows[j]; model.cpt into fd_cpt[j] when improved[j];
+//   tracking trk[j*trk_stride*2 ...] of trk_len[j] epochs into fd_trk[j].
+//   size_cpt / size_trk: current file sizes (in/out).
+// Returns 0, or the first negative errno / -1 (tracking too long) per job in
+// status[j] and the count of failed jobs as the (negative) return value.
+int32_t fedmx_write_artifacts(const float* snap, int64_t snap_stride, const int32_t* canon_idx, int32_t n_canon,
+                              const uint8_t* tpl, int64_t tpl_len, const int64_t* regions, int32_t n_regions,
+                              int32_t n_jobs, const int32_t* rows, const int32_t* improved, const int32_t* fd_cpt,
+                              const int32_t* fd_trk, int64_t* size_cpt, int64_t* size_trk, const double* trk,
+                              const int32_t* trk_len, int32_t trk_stride, int32_t* status, int32_t n_threads) {
+  if (n_jobs <= 0) return 0;
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > n_jobs) n_threads = n_jobs;
+  auto work = [&](int j0, int j1) {
+    std::vector<uint8_t> buf(tpl, tpl + tpl_len);
+    std::vector<float> canon(static_cast<size_t>(n_canon));
+    std::vector<uint8_t> pk;
+    for (int j = j0; j < j1; ++j) {
+      int st = 0;
+      if (improved[j]) {
+        const float* row = snap + static_cast<int64_t>(rows[j]) * snap_stride;
+        for (int i = 0; i < n_canon; ++i) canon[i] = row[canon_idx[i]];
+        for (int r = 0; r < n_regions; ++r) {
+          const int64_t pos = regions[3 * r], cnt = regions[3 * r + 1], off = regions[3 * r + 2];
+          std::memcpy(buf.data() + pos, canon.data() + off, static_cast<size_t>(cnt) * 4);
+        }
+        st = write_all(fd_cpt[j], buf.data(), buf.size(), &size_cpt[j]);
+      }
+      if (st == 0) {
+        if (!pickle_tracking(trk + static_cast<int64_t>(j) * trk_stride * 2, trk_len[j], pk))
+          st = -1;
+        else
+          st = write_all(fd_trk[j], pk.data(), pk.size(), &size_trk[j]);
+      }
+      status[j] = st;
+    }
+  };
+  if (n_threads == 1) {
+    work(0, n_jobs);
+  } else {
+    std::vector<std::thread> th;
+    const int per = (n_jobs + n_threads - 1) / n_threads;
+    for (int t = 0; t < n_threads; ++t) {
+      const int j0 = t * per, j1 = std::min(n_jobs, j0 + per);
+      if (j0 < j1) th.emplace_back(work, j0, j1);
+    }
+    for (auto& x : th) x.join();
+  }
+  int32_t bad = 0;
+  for (int j = 0; j < n_jobs; ++j) bad += status[j] != 0;
+  return -bad;
+}
+
+}  // extern "C"

@@ -46,3 +46,50 @@ def test_cached_artefacts_equal_plain_writes(tmp_path):
             assert open(os.path.join(a, name), "rb").read() == open(os.path.join(b, name), "rb").read()
     assert pickle.loads(open(os.path.join(a, "training_tracking.pkl"), "rb").read()) == trk
     f.close()
+
+
+def test_native_pickle_tracking_matches_pickle():
+    from fedmse_decentralized_amd.ops import _host
+
+    rng = np.random.default_rng(1)
+    for n in (0, 1, 2, 3, 7, 100, 1000):
+        trk = [(float(a), float(b)) for a, b in rng.normal(size=(n, 2))]
+        if n > 2:
+            trk[1] = (float("nan"), float("inf"))
+        assert _host.pickle_tracking(trk) == pickle.dumps(trk, protocol=4), n
+
+
+def test_native_round_writer_matches_python_writers(tmp_path):
+    """write_round_artifacts (one native call per round, threads) leaves the
+    bytes of save_model_cpt_fast / save_tracking, across rounds in which
+    files shrink and grow and some clients do not improve."""
+    import torch
+
+    from fedmse_decentralized_amd.models.layout import P_PAD, padded_index
+
+    cidx = padded_index(DEFAULT_DIMS)[0].numpy()
+    rng = np.random.default_rng(2)
+    f = ArtifactFiles()
+    n = 20
+    nat = [str(tmp_path / "nat" / f"c{i}") for i in range(n)]
+    ref = [str(tmp_path / "ref" / f"c{i}") for i in range(n)]
+    for rnd in range(4):
+        snap = torch.from_numpy(rng.normal(size=(n + 3, P_PAD)).astype(np.float32))
+        rows = rng.permutation(n + 3)[:n]
+        improved = [bool(x) for x in rng.integers(0, 2, size=n)] if rnd else [True] * n
+        trks = [[(float(a), float(b)) for a, b in rng.normal(size=(int(rng.integers(1, 6)), 2))]
+                for _ in range(n)]
+        ckpt.write_round_artifacts(f, nat, snap.numpy(), rows, improved, trks, cidx, DEFAULT_DIMS, n_threads=3)
+        for j in range(n):
+            if improved[j]:
+                ckpt.save_model_cpt_fast(ref[j], snap[rows[j]].numpy()[cidx], DEFAULT_DIMS)
+            ckpt.save_tracking(ref[j], trks[j])
+    f.close()
+    for a, b in zip(nat, ref):
+        for name in ("model.cpt", "training_tracking.pkl"):
+            assert open(os.path.join(a, name), "rb").read() == open(os.path.join(b, name), "rb").read()
+    # the reference's own reader gets the state dict back
+    import torch as _t
+
+    sd = _t.load(os.path.join(nat[0], "model.cpt"), weights_only=True)
+    assert list(sd.keys())[0] == "encoder.encoder_network.0.weight"
