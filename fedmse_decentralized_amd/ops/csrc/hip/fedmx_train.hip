@@ -50,6 +50,29 @@
 #ifndef FEDMX_SCHED_HINTS
 #define FEDMX_SCHED_HINTS 4
 #endif
+// Timing-only ablations (scripts/ab_variants.py "abl_*"; WRONG numerics, never
+// a production build): drop one piece of the step to measure what it costs
+// on the step's critical path.  1 = skip W4's gradient + Adam, 2 = skip W1's
+// Adam, 4 = skip the small tiles' Adam, 8 = skip every Adam update.
+#ifndef FEDMX_ABLATE
+#define FEDMX_ABLATE 0
+#endif
+// placement of W4's Adam update in the step (see w4_update); measured
+// (r2, 5 clients x 5 epochs): 0 1.090 ms, 1 1.117 ms, 2 1.112 ms
+#ifndef FEDMX_W4_POS
+#define FEDMX_W4_POS 0
+#endif
+// 1: scaled-moment Adam (adam4s, fedmx_train_common.h: 5 instead of 8 VALU
+// issues per parameter); 0: adam4.  Measured (r2): 1.096 vs 1.091 ms — the
+// step is bound by its dependent chain, not by VALU issue — so off by default.
+#ifndef FEDMX_ADAM_SCALED
+#define FEDMX_ADAM_SCALED 0
+#endif
+#if FEDMX_ADAM_SCALED
+#define FEDMX_ADAM4 adam4s
+#else
+#define FEDMX_ADAM4 adam4
+#endif
 
 namespace fedmx {
 
@@ -134,6 +157,20 @@ __device__ __forceinline__ void lds_to_slab(Slab& o, const Lane& L) {
       for (int v = 0; v < 2; ++v) o.q4[v][t][r] = L.w4[(16 * v + r) * S_W4 + 16 * t];
 #pragma unroll
   for (int r = 0; r < 4; ++r) o.o[r] = L.own[r * L.own_stride];
+}
+
+__device__ __forceinline__ void scale_slab(Slab& o, float f) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        o.q1[t][v][r] *= f;
+        o.q4[t][v][r] *= f;
+      }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o.o[r] *= f;
 }
 
 // 16x16 product summed over the two 16-wide halves of the hidden axis
@@ -244,6 +281,12 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   __syncthreads();
   lds_to_slab(V, L);
   __syncthreads();
+  // moment scales of the scaled-moment Adam (identity otherwise)
+  const float c1 = 1.f - A.beta1, c2 = 1.f - A.beta2;
+  if (FEDMX_ADAM_SCALED) {
+    scale_slab(M, (float)(1.0 / (double)c1));
+    scale_slab(V, (float)(1.0 / (double)c2));
+  }
   if (PROX) {
     global_to_masters_o<CP>(A.anchor + (size_t)cid * P_PAD, sW1, sW4, sW2, sW3);
     __syncthreads();
@@ -572,6 +615,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   K.one_m_b2 = 1.f - A.beta2;
   K.eps = A.eps;
   K.two_mu = 2.f * A.mu;
+  K.b1 = A.beta1;
   // beta^step as running products (python: 1 - beta ** step)
   double b1pow = pow((double)A.beta1, (double)step);
   double b2pow = pow((double)A.beta2, (double)step);
@@ -616,6 +660,11 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
         K.bc2s = (float)sqrt(1.0 - b2pow);
         K.inv_bc2s = 1.0f / K.bc2s;
+        if (FEDMX_ADAM_SCALED) {
+          const double S = -((double)A.lr / (1.0 - b1pow)) * (double)c1;
+          K.kd = (float)(sqrt((double)c2) / (sqrt(1.0 - b2pow) * S));
+          K.ed = (float)((double)A.eps / S);
+        }
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -720,18 +769,26 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         dh3[t] = s;
       }
       float prox_acc = 0.f;  // sum (p - anchor)^2 of owned params (pre-update)
-      if (last) {
-        ++step;
-        // W4 is not read again this step (its dH3 product ran before barrier
-        // #2): update it here, where its VALU work overlaps the backward MFMAs
+      // W4's Adam update + publish (its rows are read back by this wave only,
+      // by the next layer-4 product).  W4 is not read again this step (its
+      // dH3 product ran before barrier #2).  FEDMX_W4_POS places it (ONE
+      // kernels): 0 here, where its VALU work is meant to overlap the
+      // backward MFMAs; 1 after the dH1 product, 2 after the next chunk's
+      // layer-1 issue — both behind a scheduling fence, so the dependent
+      // dZ -> dH1 -> dW1 chain is issued first.
+      auto w4_update = [&]() {
+        if (FEDMX_ABLATE & 9) return;
 #pragma unroll
         for (int v = 0; v < 2; ++v)
 #pragma unroll
-          for (int t = 0; t < 2; ++t) adam4<PROX>(P.q4[v][t], M.q4[v][t], V.q4[v][t], AN.q4[v][t], G4[v][t], K, prox_acc);
-        // publish the own W4 rows now (read back by this wave only, by the
-        // next layer-4 product): the stores pin the update ahead of the
-        // wave_sync below instead of letting it sink to the step's end
+          for (int t = 0; t < 2; ++t)
+            FEDMX_ADAM4<PROX>(P.q4[v][t], M.q4[v][t], V.q4[v][t], AN.q4[v][t], G4[v][t], K, prox_acc);
         w4_to_lds(P, L);
+      };
+      constexpr int W4POS = ONE ? FEDMX_W4_POS : 0;
+      if (last) {
+        ++step;
+        if (W4POS == 0) w4_update();
       }
       // dH3^T for the owned dW3 tile (dY^T reads are done).  Written by every
       // wave (own scratch) so the step stays one basic block for the scheduler.
@@ -764,6 +821,11 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         dh1b[t] = acc;
       }
       STAMP(stamp_on, 8);
+      if (W4POS == 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        w4_update();
+        __builtin_amdgcn_sched_barrier(0);
+      }
       // ---- dW1^T (own columns) = X^T dH1: D[d=4g+r][h=c] lands in the q1 layout
 #pragma unroll
       for (int s = 0; s < KB; ++s) {
@@ -785,16 +847,23 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       STAMP(stamp_on, 9);
       if (last) {
         // W1 first: the next chunk's layer-1 product waits on it
+        if (!(FEDMX_ABLATE & 10)) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+          for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int v = 0; v < 2; ++v) adam4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
+            for (int v = 0; v < 2; ++v)
+              FEDMX_ADAM4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
+        }
         STAMP(stamp_on, 10);
         // (after an epoch's last batch this works on a stale tile; the result
         // is unused and the product stays branch-free)
         finalize_chunk(bc_n, nxt);
         l1_partial(nxt, l1a, l1b);
-        adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
+        if (W4POS == 2) {
+          __builtin_amdgcn_sched_barrier(0);
+          w4_update();
+        }
+        if (!(FEDMX_ABLATE & 12)) FEDMX_ADAM4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
         if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
         // publish the owned small tile (read by every wave after barrier #1)
         own_to_lds(P, L);
@@ -926,6 +995,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   __syncthreads();
   masters_to_global_o<CP>(Pg, sW1, sW4, sW2, sW3);
   __syncthreads();
+  if (FEDMX_ADAM_SCALED) {
+    scale_slab(M, c1);
+    scale_slab(V, c2);
+  }
   slab_to_lds(M, L);
   __syncthreads();
   masters_to_global_o<CP>(Mg, sW1, sW4, sW2, sW3);

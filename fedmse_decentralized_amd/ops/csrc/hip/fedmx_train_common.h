@@ -60,7 +60,50 @@ constexpr int STAMP_STEP = 20;
 
 struct AdamStep {
   float one_m_b1, b2, one_m_b2, inv_bc2s, bc2s, eps, neg_step_size, two_mu;
+  float b1, kd, ed;   // scaled form (adam4s)
 };
+
+// Scaled-moment Adam (fedmx_train.hip, FEDMX_ADAM_SCALED): the kernel keeps
+//   mh = m / (1-b1),  vh = v / (1-b2)
+// in registers for the whole launch (scaled on load, unscaled on write-back),
+// which turns torch's update into
+//   mh = b1*mh + g ;  vh = b2*vh + g*g ;
+//   p  = p + mh / (sqrt(vh)*kd + ed)
+// with the per-step scalars  S  = -(lr/bc1)*(1-b1),
+//   kd = sqrt(1-b2) / (sqrt(bc2)*S),  ed = eps / S
+// (algebraically torch's  p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)):
+// 5 VALU + 2 transcendental issues per parameter instead of 8 + 2 — the
+// optimizer is ~35 % of the training launch (ablation, profiles/r2_*).
+// Rounding differs from the unscaled form in the last bits only.
+template <bool PROX>
+__device__ __forceinline__ void adam4s(float (&p)[4], float (&m)[4], float (&v)[4], const float (&a)[4], f32x4 g,
+                                       const AdamStep& K, float& prox_acc) {
+  float gr[4], t0[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) gr[r] = g[r];
+  if (PROX) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) t0[r] = p[r] - a[r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) prox_acc += t0[r] * t0[r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gr[r] = gr[r] + K.two_mu * t0[r];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t0[r] = v[r] * K.b2;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(gr[r], gr[r], t0[r]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) m[r] = __builtin_fmaf(K.b1, m[r], gr[r]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t0[r] = __builtin_amdgcn_sqrtf(v[r]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t0[r] = __builtin_fmaf(t0[r], K.kd, K.ed);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t0[r] = __builtin_amdgcn_rcpf(t0[r]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p[r] = __builtin_fmaf(m[r], t0[r], p[r]);
+}
 
 // torch.optim.Adam single-tensor update (no weight decay / amsgrad):
 //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2)

@@ -25,6 +25,15 @@ VARIANTS = {
     "split": ["-DFEDMX_SPLIT_CHAINS=1"],          # L2 / dZ as two accumulator chains (+0.3%)
     "novgprform": ["-mllvm", "-amdgpu-mfma-vgpr-form=0"],  # AGPR accumulators (+3.3%)
     "noslp": ["-fno-slp-vectorize"],              # no packed fp32 VALU        (+5%)
+    "w4pos1": ["-DFEDMX_W4_POS=1"],               # W4 Adam after dH1, fenced   (+2.5%)
+    "w4pos2": ["-DFEDMX_W4_POS=2"],               # W4 Adam after the next L1 issue, fenced (+2%)
+    "scaled": ["-DFEDMX_ADAM_SCALED=1"],          # scaled-moment Adam, 5 VALU/param (+0.5%)
+    # timing-only ablations (wrong numerics): what each optimizer piece costs
+    # on the critical path (r2, base 1.095 ms)
+    "abl_w4": ["-DFEDMX_ABLATE=1"],               # no dW4 / W4 Adam          0.991 ms (-9.5%)
+    "abl_w1adam": ["-DFEDMX_ABLATE=2"],           # no W1 Adam                0.912 ms (-17%)
+    "abl_small": ["-DFEDMX_ABLATE=4"],            # no small-tile Adam        1.063 ms (-3%)
+    "abl_adam": ["-DFEDMX_ABLATE=8"],             # no Adam at all            0.708 ms (-35%)
 }
 
 
