@@ -37,6 +37,13 @@ TRAIN_WAVES = int(os.environ.get("FEDMX_TRAIN_WAVES", "4"))
 # identity order (A/B timing, cross-checks)
 TRAIN_COMPACT = os.environ.get("FEDMX_TRAIN_COMPACT", "1") != "0"
 TRAIN_FLAG_NO_COMPACT = 1
+TRAIN_FLAG_HELPER = 2
+TRAIN_FLAG_NO_HELPER = 4
+# helper-wave training kernel (fedmx_train_hw.hip: 8 waves, W4's gradient and
+# Adam on a second wave per SIMD) for the compact shapes: "1" on, "0" off,
+# unset: the library's build default
+_HELPER_ENV = os.environ.get("FEDMX_TRAIN_HELPER")
+TRAIN_HELPER = None if _HELPER_ENV is None else _HELPER_ENV != "0"
 _lib = None
 
 FWD_DTYPE = np.dtype([
@@ -566,7 +573,7 @@ class TrainBuffers:
 
 
 def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tensor] = None, waves: int = 0,
-          compact: Optional[bool] = None):
+          compact: Optional[bool] = None, helper: Optional[bool] = None):
     """Launch the fused training kernel for store rows ``local_ids`` (async).
     Returns host views (tracking[k, E, 2], epochs_run[k], best_epoch[k])
     written by the kernel, valid after the next stream sync."""
@@ -604,6 +611,9 @@ def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tens
     a.lam, a.mu = hp.shrink_lambda, hp.fedprox_mu
     a.stamps = stamps.data_ptr() if stamps is not None else None
     a.flags = 0 if (TRAIN_COMPACT if compact is None else compact) else TRAIN_FLAG_NO_COMPACT
+    helper_on = TRAIN_HELPER if helper is None else helper
+    if helper_on is not None:
+        a.flags |= TRAIN_FLAG_HELPER if helper_on else TRAIN_FLAG_NO_HELPER
     # the 8-wave variant covers single-tile batches only
     if hp.batch_size <= 16 and (waves or TRAIN_WAVES) == 8:
         rc = lib().fedmx_train8(ctypes.byref(a), k, rt.stream)

@@ -38,6 +38,8 @@ struct TrainArgs {
   int32_t pad0;
 };
 constexpr int32_t TRAIN_FLAG_NO_COMPACT = 1;  // identity-order kernels even where the compact order applies
+constexpr int32_t TRAIN_FLAG_HELPER = 2;      // helper-wave kernel (fedmx_train_hw.hip) for the compact shapes
+constexpr int32_t TRAIN_FLAG_NO_HELPER = 4;   // never the helper-wave kernel
 
 // In-kernel phase timestamps (build with -DFEDMX_STAMPS=1): wave w's lane 0 of
 // workgroup 0 records s_memtime at fixed points of training step STAMP_STEP

@@ -1,0 +1,838 @@
+// Persistent fused local training with HELPER WAVES (gfx950, 8 wave64 per
+// client: two per SIMD).  Same math, same per-lane data layouts and the same
+// results as train_kernel<PROX, ONE=true, CP=true> (fedmx_train.hip), for the
+// reference shapes (batch <= 12, hidden <= 27, latent <= 7).
+//
+// Why: one wave per SIMD exposes every dependency stall of the step's serial
+// chain L1 -> L2 -> L3 -> L4 -> dH3 -> dZ -> dH1 -> dW1 -> Adam(W1) -> L1.
+// Timing ablations of fedmx_train.hip (scripts/ab_variants.py abl_*) put the
+// W4 gradient + Adam work at ~9.5 % of the launch although nothing on the
+// chain waits for it before the next step's layer 4.  Here that work moves to
+// a second wave on each SIMD, which issues while the first one stalls:
+//
+//   waves 0..3 ("main", one per SIMD): the chain exactly as in train_kernel,
+//     minus dW4 / W4's Adam.  W4's rows come back each step from LDS (the
+//     master for layer 4 as before, plus a copy in the dH3 A-operand layout).
+//   waves 4..7 ("helper" h, on the SIMD of main w = h - 4): own W4 rows
+//     [32w, 32w+32) with their Adam state (param, m, v, FedProx anchor) in
+//     registers.  Between barrier #2 of step s and barrier #1 of step s+1 a
+//     helper reads main w's dY^T / H3^T tiles, forms dW4 (12 MFMAs), runs the
+//     Adam update and publishes W4(s+1) (master rows + A-operand copy).  The
+//     two workgroup barriers of the step are the only synchronisation.
+//   validation: all 8 waves share the epoch's validation batches.
+//
+// Barrier sequence (every wave executes exactly this): prologue staging
+// (2 per state tensor), per training step #1 / #2, per epoch: masters
+// published, loss exchange, snapshot; epilogue write-back.
+#include "fedmx_train_common.h"
+
+// issue priority of the main waves over their helpers (s_setprio level; 0: equal)
+#ifndef FEDMX_HW_PRIO
+#define FEDMX_HW_PRIO 0
+#endif
+
+namespace fedmx {
+namespace hw {
+
+constexpr int L_W1 = HP * S_W1;          // 4224
+constexpr int L_W4 = DP * S_W4;          // 4608
+constexpr int L_W2 = ZP * S_W2;          // 576
+constexpr int L_W3 = HP * S_W3;          // 640
+constexpr int L_RED = 4 * 2 * 64 * 4;    // 2048
+constexpr int L_T32 = 32 * S_T;          // 640
+constexpr int L_T16 = 16 * S_T;          // 320
+constexpr int L_SCR = 4 * L_T32 + 2 * L_T16;  // 3200 per main wave (dY^T, H3^T, H1^T, dH3^T | Z^T, dZ^T)
+constexpr int L_Q4 = 4 * 4 * 64 * 4;     // 4096 W4 rows in the dH3 A-operand layout [w][v][t][lane][4]
+constexpr int L_TOTAL = L_W1 + L_W4 + L_W2 + L_W3 + 3 * L_RED + 4 * L_SCR + L_Q4 + 128;
+static_assert(L_TOTAL * 4 <= 160 * 1024, "LDS budget");
+
+// main-wave optimizer state: W1 column block (MFMA A-operand layout) + small tile
+struct MSlab {
+  float q1[2][2][4];
+  float o[4];
+};
+// helper-wave optimizer state: W4 row block (D layout, see fedmx_train.hip)
+struct HSlab {
+  float q4[2][2][4];
+};
+
+struct Lane {
+  float* w1;   // sW1 + c*S_W1 + 32w + 4g
+  float* w4;   // sW4 + (32w+4g)*S_W4 + c
+  float* own;
+  int own_stride;
+};
+
+__device__ __forceinline__ void w1_to_lds(const MSlab& o, const Lane& L) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+      lds_write4(L.w1 + 16 * t * S_W1 + 16 * v, f32x4{o.q1[t][v][0], o.q1[t][v][1], o.q1[t][v][2], o.q1[t][v][3]});
+}
+__device__ __forceinline__ void own_to_lds(const MSlab& o, const Lane& L) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) L.own[r * L.own_stride] = o.o[r];
+}
+__device__ __forceinline__ void lds_to_mslab(MSlab& o, const Lane& L) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const f32x4 q = lds_read4(L.w1 + 16 * t * S_W1 + 16 * v);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o.q1[t][v][r] = q[r];
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o.o[r] = L.own[r * L.own_stride];
+}
+__device__ __forceinline__ void w4_to_lds(const HSlab& o, const Lane& L) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) L.w4[(16 * v + r) * S_W4 + 16 * t] = o.q4[v][t][r];
+}
+__device__ __forceinline__ void lds_to_hslab(HSlab& o, const Lane& L) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) o.q4[v][t][r] = L.w4[(16 * v + r) * S_W4 + 16 * t];
+}
+
+// compact-order product over the two halves of the hidden axis (7 k-steps)
+__device__ __forceinline__ f32x4 chain2(f32x4 a0, f32x4 a1, f32x4 b0, f32x4 b1) {
+  f32x4 x = zero4();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) x = mfma16(a0[s], b0[s], x);
+#pragma unroll
+  for (int s = 0; s < 3; ++s) x = mfma16(a1[s], b1[s], x);
+  return x;
+}
+
+struct XChunk {
+  f32x4 f0, f1, b0, b1;
+};
+
+template <bool PROX>
+__global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
+  constexpr bool CP = true;
+  constexpr int KB = 3;   // k-steps of products over the batch (compact order)
+  constexpr int KZ = 2;   // k-steps of products over the latent axis
+  __shared__ __attribute__((aligned(16))) float lds[L_TOTAL];
+  const int w8 = threadIdx.x >> 6;
+  const bool helper = w8 >= 4;
+  const int w = w8 & 3;           // main wave index / the main wave a helper serves
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 15;
+  const int g = lane >> 4;
+  const bool stager = threadIdx.x < 256;
+  float* const sW1 = lds;
+  float* const sW4 = sW1 + L_W1;
+  float* const sW2 = sW4 + L_W4;
+  float* const sW3 = sW2 + L_W2;
+  float* const sRedH1 = sW3 + L_W3;               // two buffers (parity)
+  float* const sRedDH3 = sRedH1 + 2 * L_RED;
+  float* const scr = sRedDH3 + L_RED + w * L_SCR;
+  float* const sT0 = scr;                // dY^T own rows   (main -> helper)
+  float* const sT1 = sT0 + L_T32;        // H3^T            (main -> helper)
+  float* const sH1T = sT1 + L_T32;       // H1^T
+  float* const sT2 = sH1T + L_T32;       // dH3^T
+  float* const sZT = sT2 + L_T32;        // Z^T (with bias row)
+  float* const sDZT = sZT + L_T16;       // dZ^T
+  float* const sQ4 = sRedDH3 + L_RED + 4 * L_SCR;   // [w][v][t][lane][4]
+  double* const sLoss = reinterpret_cast<double*>(sQ4 + L_Q4);  // [8 waves][4]
+
+  Lane L;
+  L.w1 = sW1 + c * S_W1 + 32 * w + 4 * g;
+  L.w4 = sW4 + (32 * w + 4 * g) * S_W4 + c;
+  if (w < 2) {
+    L.own = sW3 + (16 * w + 4 * g) * S_W3 + c;
+    L.own_stride = S_W3;
+  } else {
+    L.own = sW2 + 4 * g * S_W2 + 16 * (w - 2) + c;
+    L.own_stride = S_W2;
+  }
+  float* const q4p = sQ4 + (w * 4 * 64 + lane) * 4;   // + (2v + t) * 256
+  const float* const a4p = sW4 + (32 * w + c) * S_W4 + 4 * g;
+  const float* const a2p = sW2 + c * S_W2 + 4 * g;
+  const float* const a3p = sW3 + c * S_W3 + 4 * g;
+  const float* const d2p = sW2 + 4 * g * S_W2 + c;
+  const float* const d3p = sW3 + 4 * g * S_W3 + c;
+  const int tw = 4 * g * S_T + c;
+  const int tr = c * S_T + 4 * g;
+  float* const redw = sRedDH3 + (w * 2) * 256 + lane * 4;
+
+  const int kslot = blockIdx.x;
+  const int cid = A.client_idx[kslot];
+  float* const Pg = A.params + (size_t)cid * P_PAD;
+  float* const Mg = A.adam_m + (size_t)cid * P_PAD;
+  float* const Vg = A.adam_v + (size_t)cid * P_PAD;
+  float* const Bg = A.best + (size_t)cid * P_PAD;
+  const int d_in = A.d_in, hidden = A.hidden, latent = A.latent;
+
+  const int B = A.batch;
+  const float* const Xtr = A.train_x + (size_t)A.train_off[cid] * DP;
+  const int n_tr = (int)(A.train_off[cid + 1] - A.train_off[cid]);
+  const float* const Xva = A.valid_x + (size_t)A.valid_off[cid] * DP;
+  const int n_va = (int)(A.valid_off[cid + 1] - A.valid_off[cid]);
+  const int nb = (n_tr + B - 1) / B;
+  const int nvb = (n_va + B - 1) / B;
+  int step = A.adam_step[cid];
+  int parity = 0;
+  const bool bias_lane = (w == 3 && g == 3);
+  const bool bias_col = (w == 3 && c == 15);
+  const int xcol = 32 * w + 4 * g;
+  const float lam = A.lambda;
+  const float inv_d = 1.0f / (float)d_in;
+  bool hreal_d[2][4], hbias_d[2][4], zreal_d[4], zbias_d[4], hreal_c[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = hslot_of_pos<CP>(16 * t + 4 * g + r);
+      hreal_d[t][r] = j < hidden;
+      hbias_d[t][r] = j == h_bias_slot<CP>();
+    }
+    hreal_c[t] = hslot_of_pos<CP>(16 * t + c) < hidden;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = zslot_of_pos<CP>(4 * g + r);
+    zreal_d[r] = j < latent;
+    zbias_d[r] = j == z_bias_slot<CP>();
+  }
+  const int brow_c = batch_row_of_col<CP>(c);
+  int brow_b[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) brow_b[r] = batch_row_of_col<CP>(4 * g + r);
+
+  auto load_chunk = [&](const float* X, int row0, int bc, XChunk& x) {
+    const float* src = X + (size_t)(row0 + ((unsigned)brow_c < (unsigned)bc ? brow_c : 0)) * DP + xcol;
+    x.f0 = *reinterpret_cast<const f32x4*>(src);
+    x.f1 = *reinterpret_cast<const f32x4*>(src + 16);
+    const float* bsrc = X + (size_t)row0 * DP + 32 * w + c;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {   // row quad 3 is padding, never read
+      const int rr = ((unsigned)brow_b[r] < (unsigned)bc) ? brow_b[r] : 0;
+      x.b0[r] = bsrc[(size_t)rr * DP];
+      x.b1[r] = bsrc[(size_t)rr * DP + 16];
+    }
+    x.b0[3] = 0.f;
+    x.b1[3] = 0.f;
+  };
+  auto finalize_chunk = [&](XChunk& x) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+      if (bias_col) x.b1[r] = 1.f;
+    if (bias_lane) x.f1[3] = 1.f;
+  };
+  // whole forward of one validation chunk by one wave (any of the 8), exactly
+  // as fedmx_train.hip's valid_chunk
+  auto valid_chunk = [&](const float* X, int row0, int bc, float inv_bt, double& lacc) {
+    asm volatile("" ::: "memory");
+    const bool ok = (unsigned)brow_c < (unsigned)bc;
+    const float* src = X + (size_t)(row0 + (ok ? brow_c : 0)) * DP + 4 * g;
+    f32x4 xf[4][2];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const f32x4 q = *reinterpret_cast<const f32x4*>(src + 32 * b + 16 * v);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xf[b][v][r] = q[r];
+      }
+    if (g == 3) xf[3][1][3] = 1.f;
+    f32x4 h1[2];
+    {
+      f32x4 sum0 = zero4(), sum1 = zero4();
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        f32x4 p0 = zero4(), p1 = zero4();
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const f32x4 a0 = lds_read4(sW1 + c * S_W1 + 32 * b + 16 * v + 4 * g);
+          const f32x4 a1 = lds_read4(sW1 + (16 + c) * S_W1 + 32 * b + 16 * v + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            p0 = mfma16(a0[r], xf[b][v][r], p0);
+            p1 = mfma16(a1[r], xf[b][v][r], p1);
+          }
+        }
+        if (b == 0) {
+          sum0 = p0;
+          sum1 = p1;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            sum0[r] = sum0[r] + p0[r];
+            sum1[r] = sum1[r] + p1[r];
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v0 = fmaxf(sum0[r], 0.f), v1 = fmaxf(sum1[r], 0.f);
+        if (hbias_d[0][r]) v0 = 1.f;
+        if (hbias_d[1][r]) v1 = 1.f;
+        sum0[r] = v0;
+        sum1[r] = v1;
+      }
+      h1[0] = sum0;
+      h1[1] = sum1;
+    }
+    const f32x4 z = chain2(lds_read4(a2p), lds_read4(a2p + 16), h1[0], h1[1]);
+    f32x4 zb = z;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (zbias_d[r]) zb[r] = 1.f;
+    f32x4 h3[2];
+    {
+      f32x4 acc0 = zero4(), acc1 = zero4();
+      const f32x4 a0 = lds_read4(a3p);
+      const f32x4 a1 = lds_read4(a3p + 16 * S_W3);
+#pragma unroll
+      for (int s = 0; s < KZ; ++s) {
+        acc0 = mfma16(a0[s], zb[s], acc0);
+        acc1 = mfma16(a1[s], zb[s], acc1);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v0 = fmaxf(acc0[r], 0.f), v1 = fmaxf(acc1[r], 0.f);
+        if (hbias_d[0][r]) v0 = 1.f;
+        if (hbias_d[1][r]) v1 = 1.f;
+        acc0[r] = v0;
+        acc1[r] = v1;
+      }
+      h3[0] = acc0;
+      h3[1] = acc1;
+    }
+    float nz = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) nz += zreal_d[r] ? z[r] * z[r] : 0.f;
+    nz = sum_lane_groups(nz);
+    const float norm_v = __builtin_amdgcn_sqrtf(nz);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      f32x4 acc0 = zero4(), acc1 = zero4();
+      const float* ap = sW4 + (32 * b + c) * S_W4 + 4 * g;
+      const f32x4 a00 = lds_read4(ap);
+      const f32x4 a01 = lds_read4(ap + 16);
+      const f32x4 a10 = lds_read4(ap + 16 * S_W4);
+      const f32x4 a11 = lds_read4(ap + 16 * S_W4 + 16);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc0 = mfma16(a00[s], h3[0][s], acc0);
+        acc1 = mfma16(a10[s], h3[0][s], acc1);
+      }
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        acc0 = mfma16(a01[s], h3[1][s], acc0);
+        acc1 = mfma16(a11[s], h3[1][s], acc1);
+      }
+      float sq = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d0 = acc0[r] - xf[b][0][r];
+        const float d1 = (b == 3 && g == 3 && r == 3) ? 0.f : acc1[r] - xf[b][1][r];
+        sq += d0 * d0 + d1 * d1;
+      }
+      sq = ok ? sq : 0.f;
+      float contrib = sq * (inv_bt * inv_d);
+      if (b == 0 && g == 0 && ok) contrib += lam * norm_v * inv_bt;
+      lacc += (double)contrib;
+    }
+  };
+
+  AdamStep K;
+  K.one_m_b1 = 1.f - A.beta1;
+  K.b2 = A.beta2;
+  K.one_m_b2 = 1.f - A.beta2;
+  K.eps = A.eps;
+  K.two_mu = 2.f * A.mu;
+  double b1pow = pow((double)A.beta1, (double)step);
+  double b2pow = pow((double)A.beta2, (double)step);
+  auto next_constants = [&]() {
+    b1pow *= (double)A.beta1;
+    b2pow *= (double)A.beta2;
+    K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
+    K.bc2s = (float)sqrt(1.0 - b2pow);
+    K.inv_bc2s = 1.0f / K.bc2s;
+  };
+
+  double min_valid = __builtin_huge_val();
+  int worse = 0, ep_run = 0, best_ep = -1;
+
+  // Epoch tail, identical barrier sequence for both roles: validation (wave
+  // w8 takes batches w8, w8+8, ...), fixed-order loss exchange, tracking,
+  // patience decision, best-validation snapshot.  True: stop training.
+  auto epoch_tail = [&](int ep, double acc_tr, double prox_now) -> bool {
+    __syncthreads();   // masters published (W1 by mains, W4 by helpers, small tiles)
+    double acc_va = 0.0;
+    for (int vb = w8; vb < nvb; vb += 8) {
+      const int row0 = vb * B;
+      const int bt = min(B, n_va - row0);
+      valid_chunk(Xva, row0, bt, 1.0f / (float)bt, acc_va);
+    }
+    {
+      const double s0 = wave_sum_d(acc_tr);
+      const double s1 = wave_sum_d(acc_va);
+      const double s2 = wave_sum_d(prox_now);
+      if (lane == 0) {
+        sLoss[w8 * 4 + 0] = s0;
+        sLoss[w8 * 4 + 1] = s1;
+        sLoss[w8 * 4 + 2] = s2;
+      }
+    }
+    __syncthreads();
+    double tr_sum = 0.0, va_sum = 0.0, px_sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      tr_sum += sLoss[i * 4 + 0];
+      va_sum += sLoss[i * 4 + 1];
+      px_sum += sLoss[i * 4 + 2];
+    }
+    const double train_loss = nb > 0 ? tr_sum / nb : __builtin_nan("");
+    double valid_loss = nvb > 0 ? va_sum / nvb : __builtin_nan("");
+    if (PROX) valid_loss += (double)A.mu * px_sum;
+    if (threadIdx.x == 0) {
+      double* trk = A.tracking + ((size_t)kslot * A.epochs + ep) * 2;
+      trk[0] = train_loss;
+      trk[1] = valid_loss;
+    }
+    ep_run = ep + 1;
+    if (valid_loss < min_valid) {
+      min_valid = valid_loss;
+      best_ep = ep;
+      worse = 0;
+      if (stager) masters_to_global_o<CP>(Bg, sW1, sW4, sW2, sW3);  // save_model(): best snapshot
+    } else {
+      ++worse;
+    }
+    __syncthreads();   // sLoss reuse / masters stable for the snapshot copy
+    return worse >= A.patience && worse > 0;
+  };
+  auto stage = [&](const float* src) {
+    if (stager) global_to_masters_o<CP>(src, sW1, sW4, sW2, sW3);
+    __syncthreads();
+  };
+
+  if (helper) {
+    // =========================== helper waves ===================================
+    if (FEDMX_HW_PRIO) __builtin_amdgcn_s_setprio(0);
+    HSlab P4, M4, V4, AN4;
+    stage(Mg);
+    lds_to_hslab(M4, L);
+    __syncthreads();
+    stage(Vg);
+    lds_to_hslab(V4, L);
+    __syncthreads();
+    if (PROX) {
+      stage(A.anchor + (size_t)cid * P_PAD);
+      lds_to_hslab(AN4, L);
+      __syncthreads();
+    }
+    stage(Pg);
+    lds_to_hslab(P4, L);
+    auto publish_q4 = [&]() {
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          lds_write4(q4p + (2 * v + t) * 256, f32x4{P4.q4[v][t][0], P4.q4[v][t][1], P4.q4[v][t][2], P4.q4[v][t][3]});
+    };
+    publish_q4();
+    for (int ep = 0; ep < A.epochs; ++ep) {
+      double acc_tr = 0.0;
+      // W4 gradient + Adam between barrier #2 of step s and barrier #1 of s+1
+      for (int bi = 0; bi < nb; ++bi) {
+        next_constants();
+        __syncthreads();   // barrier #1 (main: layer-1 partials)
+        __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
+        const f32x4 w4a0 = lds_read4(sT0 + tr);
+        const f32x4 w4a1 = lds_read4(sT0 + tr + 16 * S_T);
+        const f32x4 w4b0 = lds_read4(sT1 + tr);
+        const f32x4 w4b1 = lds_read4(sT1 + tr + 16 * S_T);
+        f32x4 G4[2][2];
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) G4[v][t] = zero4();
+#pragma unroll
+        for (int s = 0; s < KB; ++s) {
+          G4[0][0] = mfma16(w4a0[s], w4b0[s], G4[0][0]);
+          G4[0][1] = mfma16(w4a0[s], w4b1[s], G4[0][1]);
+          G4[1][0] = mfma16(w4a1[s], w4b0[s], G4[1][0]);
+          G4[1][1] = mfma16(w4a1[s], w4b1[s], G4[1][1]);
+        }
+        float prox_acc = 0.f;
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            adam4<PROX>(P4.q4[v][t], M4.q4[v][t], V4.q4[v][t], AN4.q4[v][t], G4[v][t], K, prox_acc);
+        if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
+        // publish W4(s+1): master rows (layer 4, validation, snapshots) and the
+        // dH3 A-operand copy; main w reads both after barrier #1 of step s+1
+        w4_to_lds(P4, L);
+        publish_q4();
+      }
+      double prox_now = 0.0;
+      if (PROX) {
+        float pr = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+              const float d4 = P4.q4[v][t][r] - AN4.q4[v][t][r];
+              pr += d4 * d4;
+            }
+        prox_now = (double)pr;
+      }
+      if (epoch_tail(ep, acc_tr, prox_now)) break;
+    }
+    // write back (barriers as the main branch; the mains stage to global)
+    __syncthreads();
+    __syncthreads();
+    w4_to_lds(M4, L);
+    __syncthreads();
+    __syncthreads();
+    w4_to_lds(V4, L);
+    __syncthreads();
+    return;
+  }
+
+  // ============================= main waves =====================================
+  // (FEDMX_HW_PRIO: the chain's wave wins issue arbitration against its helper)
+  if (FEDMX_HW_PRIO) __builtin_amdgcn_s_setprio(FEDMX_HW_PRIO);
+  MSlab P, M, V, AN;
+  stage(Mg);
+  lds_to_mslab(M, L);
+  __syncthreads();
+  stage(Vg);
+  lds_to_mslab(V, L);
+  __syncthreads();
+  if (PROX) {
+    stage(A.anchor + (size_t)cid * P_PAD);
+    lds_to_mslab(AN, L);
+    __syncthreads();
+  }
+  stage(Pg);
+  lds_to_mslab(P, L);   // W2/W3/W4 masters stay live; W1 lives in registers only
+
+  auto l1_partial = [&](const XChunk& x, f32x4& acc0, f32x4& acc1) {
+    acc0 = zero4();
+    acc1 = zero4();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc0 = mfma16(P.q1[0][0][j], x.f0[j], acc0);
+      acc1 = mfma16(P.q1[1][0][j], x.f0[j], acc1);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc0 = mfma16(P.q1[0][1][j], x.f1[j], acc0);
+      acc1 = mfma16(P.q1[1][1][j], x.f1[j], acc1);
+    }
+  };
+
+  for (int ep = 0; ep < A.epochs; ++ep) {
+    double acc_tr = 0.0;
+    XChunk cur, nxt;
+    f32x4 l1a = zero4(), l1b = zero4();
+    if (nb > 0) {
+      load_chunk(Xtr, 0, min(B, n_tr), cur);
+      finalize_chunk(cur);
+      l1_partial(cur, l1a, l1b);
+    }
+    for (int bi = 0; bi < nb; ++bi) {
+      const int row_b = bi * B;
+      const int bt = min(B, n_tr - row_b);
+      const bool has_next = bi + 1 < nb;
+      const int row_n = (bi + 1) * B;
+      const int bc_n = has_next ? min(B, n_tr - row_n) : 0;
+      const float inv_bt = 1.0f / (float)bt;
+      next_constants();
+      f32x4 G1[2][2], Go = zero4();
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) G1[t][v] = zero4();
+
+      // ---- forward: layer-1 K reduction (barrier #1), layers 2-4, loss
+      f32x4 h1[2], z, zb, h3[2], y[2], q4[2][2];
+      float norm_c;
+      {
+        float* red = sRedH1 + parity * L_RED;
+        lds_write4(red + (w * 2 + 0) * 256 + lane * 4, l1a);
+        lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1b);
+        __syncthreads();  // barrier #1
+        // W4(s) rows in the dH3 A-operand layout (helper-published)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) q4[v][t] = lds_read4(q4p + (2 * v + t) * 256);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          f32x4 s = lds_read4(red + t * 256 + lane * 4);
+#pragma unroll
+          for (int ww = 1; ww < 4; ++ww) {
+            const f32x4 o = lds_read4(red + (ww * 2 + t) * 256 + lane * 4);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[r] = s[r] + o[r];
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float vv = fmaxf(s[r], 0.f);
+            if (hbias_d[t][r]) vv = 1.f;
+            s[r] = vv;
+          }
+          h1[t] = s;
+        }
+        parity ^= 1;
+        z = chain2(lds_read4(a2p), lds_read4(a2p + 16), h1[0], h1[1]);
+        zb = z;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (zbias_d[r]) zb[r] = 1.f;
+        {
+          f32x4 acc0 = zero4(), acc1 = zero4();
+          const f32x4 a0 = lds_read4(a3p);
+          const f32x4 a1 = lds_read4(a3p + 16 * S_W3);
+#pragma unroll
+          for (int s = 0; s < KZ; ++s) {
+            acc0 = mfma16(a0[s], zb[s], acc0);
+            acc1 = mfma16(a1[s], zb[s], acc1);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v0 = fmaxf(acc0[r], 0.f), v1 = fmaxf(acc1[r], 0.f);
+            if (hbias_d[0][r]) v0 = 1.f;
+            if (hbias_d[1][r]) v1 = 1.f;
+            acc0[r] = v0;
+            acc1[r] = v1;
+          }
+          h3[0] = acc0;
+          h3[1] = acc1;
+        }
+        {
+          f32x4 acc0 = zero4(), acc1 = zero4();
+          const f32x4 a00 = lds_read4(a4p);
+          const f32x4 a01 = lds_read4(a4p + 16);
+          const f32x4 a10 = lds_read4(a4p + 16 * S_W4);
+          const f32x4 a11 = lds_read4(a4p + 16 * S_W4 + 16);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            acc0 = mfma16(a00[s], h3[0][s], acc0);
+            acc1 = mfma16(a10[s], h3[0][s], acc1);
+          }
+#pragma unroll
+          for (int s = 0; s < 3; ++s) {
+            acc0 = mfma16(a01[s], h3[1][s], acc0);
+            acc1 = mfma16(a11[s], h3[1][s], acc1);
+          }
+          y[0] = acc0;
+          y[1] = acc1;
+        }
+        float sq = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d0 = y[0][r] - cur.f0[r];
+          const float d1 = (bias_lane && r == 3) ? 0.f : y[1][r] - cur.f1[r];
+          sq += d0 * d0 + d1 * d1;
+        }
+        const bool col_ok = (unsigned)brow_c < (unsigned)bt;
+        sq = col_ok ? sq : 0.f;
+        float nz = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) nz += zreal_d[r] ? z[r] * z[r] : 0.f;
+        nz = sum_lane_groups(nz);
+        norm_c = __builtin_amdgcn_sqrtf(nz);
+        float contrib = sq * (inv_bt * inv_d);
+        if (w == 0 && g == 0 && col_ok) contrib += lam * norm_c * inv_bt;
+        acc_tr += (double)contrib;
+      }
+      if (has_next) load_chunk(Xtr, row_n, bc_n, nxt);  // prefetch
+
+      float q2[2][4], q3[2][4];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          q2[t][r] = d2p[r * S_W2 + 16 * t];
+          q3[t][r] = d3p[(16 * t + r) * S_W3];
+        }
+
+      // ---- dY (masked, feature-major); dY^T / H3^T for the helper's dW4
+      const bool col_ok = (unsigned)brow_c < (unsigned)bt;
+      const float scale = col_ok ? 2.0f / (float)(bt * d_in) : 0.f;
+      f32x4 dy[2];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dy[0][r] = (y[0][r] - cur.f0[r]) * scale;
+        dy[1][r] = (bias_lane && r == 3) ? 0.f : (y[1][r] - cur.f1[r]) * scale;
+        sT0[tw + r * S_T] = dy[0][r];
+        sT0[tw + (16 + r) * S_T] = dy[1][r];
+        sT1[tw + r * S_T] = h3[0][r];
+        sT1[tw + (16 + r) * S_T] = h3[1][r];
+      }
+      // ---- dH3 partial = W4a(own rows)^T dY(own rows)   (W4(s))
+      {
+        f32x4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            acc0 = mfma16(q4[v][0][s], dy[v][s], acc0);
+            acc1 = mfma16(q4[v][1][s], dy[v][s], acc1);
+          }
+        lds_write4(redw, acc0);
+        lds_write4(redw + 256, acc1);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sH1T[tw + r * S_T] = h1[0][r];
+        sH1T[tw + (16 + r) * S_T] = h1[1][r];
+        sZT[tw + r * S_T] = zb[r];
+      }
+      __syncthreads();  // barrier #2: dH3 partials of all waves visible
+      f32x4 dh3[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 s = lds_read4(sRedDH3 + t * 256 + lane * 4);
+#pragma unroll
+        for (int ww = 1; ww < 4; ++ww) {
+          const f32x4 o = lds_read4(sRedDH3 + (ww * 2 + t) * 256 + lane * 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[r] = s[r] + o[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[r] = (hreal_d[t][r] && h3[t][r] > 0.f) ? s[r] : 0.f;
+        dh3[t] = s;
+      }
+      float prox_acc = 0.f;
+      ++step;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sT2[tw + (16 * t + r) * S_T] = dh3[t][r];
+      // ---- dZ = W3a^T dH3 (+ shrink-loss gradient)
+      f32x4 dz = chain2(f32x4{q3[0][0], q3[0][1], q3[0][2], q3[0][3]},
+                        f32x4{q3[1][0], q3[1][1], q3[1][2], q3[1][3]}, dh3[0], dh3[1]);
+      const float shr_raw = lam * __builtin_amdgcn_rcpf((float)bt * norm_c);
+      const float shr = (col_ok && norm_c > 0.f) ? shr_raw : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dz[r] = zreal_d[r] ? dz[r] + shr * z[r] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sDZT[tw + r * S_T] = dz[r];
+      // ---- dH1 (batch-major) with the ReLU mask from H1^T
+      f32x4 dh1b[2], h1b[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        h1b[t] = lds_read4(sH1T + tr + 16 * t * S_T);
+        f32x4 acc = zero4();
+#pragma unroll
+        for (int s = 0; s < KZ; ++s) acc = mfma16(dz[s], q2[t][s], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = (hreal_c[t] && h1b[t][r] > 0.f) ? acc[r] : 0.f;
+        dh1b[t] = acc;
+      }
+      // ---- dW1^T (own columns) = X^T dH1
+#pragma unroll
+      for (int s = 0; s < KB; ++s) {
+        G1[0][0] = mfma16(cur.b0[s], dh1b[0][s], G1[0][0]);
+        G1[0][1] = mfma16(cur.b1[s], dh1b[0][s], G1[0][1]);
+        G1[1][0] = mfma16(cur.b0[s], dh1b[1][s], G1[1][0]);
+        G1[1][1] = mfma16(cur.b1[s], dh1b[1][s], G1[1][1]);
+      }
+      wave_sync();
+      // ---- owned small tile: w<2 -> dW3 tile = dH3^T Z ; w>=2 -> dW2 tile = dZ^T H1
+      {
+        const f32x4 a = lds_read4(w < 2 ? sT2 + tr + 16 * w * S_T : sDZT + tr);
+        const f32x4 bz = lds_read4(sZT + tr);
+        const f32x4 b = (w < 2) ? bz : ((w == 2) ? h1b[0] : h1b[1]);
+#pragma unroll
+        for (int s = 0; s < KB; ++s) Go = mfma16(a[s], b[s], Go);
+      }
+      // W1 first: the next chunk's layer-1 product waits on it
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) adam4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
+      // (after an epoch's last batch this works on a stale tile; unused)
+      finalize_chunk(nxt);
+      l1_partial(nxt, l1a, l1b);
+      adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
+      if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
+      own_to_lds(P, L);   // read by every wave after barrier #1
+      __builtin_amdgcn_iglp_opt(0);
+      cur = nxt;
+    }
+    w1_to_lds(P, L);   // W1 master (validation, snapshot)
+    double prox_now = 0.0;
+    if (PROX) {
+      float pr = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int v = 0; v < 2; ++v) {
+            const float d1 = P.q1[t][v][r] - AN.q1[t][v][r];
+            pr += d1 * d1;
+          }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = P.o[r] - AN.o[r];
+        pr += d * d;
+      }
+      prox_now = (double)pr;
+    }
+    if (epoch_tail(ep, acc_tr, prox_now)) break;
+  }
+
+  // ---- write back: params (masters), then m and v through the same staging
+  __syncthreads();
+  masters_to_global_o<CP>(Pg, sW1, sW4, sW2, sW3);
+  __syncthreads();
+  w1_to_lds(M, L);
+  own_to_lds(M, L);
+  __syncthreads();
+  masters_to_global_o<CP>(Mg, sW1, sW4, sW2, sW3);
+  __syncthreads();
+  w1_to_lds(V, L);
+  own_to_lds(V, L);
+  __syncthreads();
+  masters_to_global_o<CP>(Vg, sW1, sW4, sW2, sW3);
+  if (threadIdx.x == 0) {
+    A.adam_step[cid] = step;
+    A.epochs_run[kslot] = ep_run;
+    A.best_epoch[kslot] = best_ep;
+  }
+}
+
+}  // namespace hw
+}  // namespace fedmx
+
+extern "C" {
+
+// Helper-wave training launch for the compact reference shapes; returns -4
+// when the shapes need the general kernel (fedmx_train).
+int fedmx_train_hw(const void* args, int k, hipStream_t stream) {
+  if (k <= 0) return 0;
+  const fedmx::TrainArgs& A = *reinterpret_cast<const fedmx::TrainArgs*>(args);
+  if (!(A.batch >= 1 && A.batch <= 12 && A.d_in >= 1 && A.d_in <= fedmx::DP - 1 && A.hidden >= 1 &&
+        A.hidden <= 27 && A.latent >= 1 && A.latent <= 7))
+    return -4;
+  if (A.mu != 0.f)
+    hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true>), dim3(k), dim3(512), 0, stream, A);
+  else
+    hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<false>), dim3(k), dim3(512), 0, stream, A);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

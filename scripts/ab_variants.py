@@ -27,6 +27,9 @@ VARIANTS = {
     "noslp": ["-fno-slp-vectorize"],              # no packed fp32 VALU        (+5%)
     "w4pos1": ["-DFEDMX_W4_POS=1"],               # W4 Adam after dH1, fenced   (+2.5%)
     "w4pos2": ["-DFEDMX_W4_POS=2"],               # W4 Adam after the next L1 issue, fenced (+2%)
+    "nohw": ["-DFEDMX_TRAIN_HW_DEFAULT=0"],       # 4-wave kernel for the compact shapes too (+3%, FedProx +8%)
+    "hwprio1": ["-DFEDMX_HW_PRIO=1"],             # main waves at issue priority 1 over helpers (+0.4%)
+    "hwprio3": ["-DFEDMX_HW_PRIO=3"],             # main waves at issue priority 3 (+0.4%)
     "scaled": ["-DFEDMX_ADAM_SCALED=1"],          # scaled-moment Adam, 5 VALU/param (+0.5%)
     # timing-only ablations (wrong numerics): what each optimizer piece costs
     # on the critical path (r2, base 1.095 ms)

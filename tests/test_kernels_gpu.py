@@ -171,6 +171,33 @@ def test_train_kernel_compact_order_matches_identity_order(batch, lam, mu):
         assert torch.count_nonzero(getattr(a.store, name)[:, pad]) == 0
 
 
+@pytest.mark.parametrize("batch,lam,mu,epochs,patience", [(12, 5.0, 0.0, 4, 1), (7, 1.0, 0.001, 3, 1),
+                                                           (1, 5.0, 0.0, 2, 1), (12, 0.0, 0.01, 5, 10 ** 6)])
+def test_train_kernel_helper_waves_match_four_waves(batch, lam, mu, epochs, patience):
+    """The helper-wave kernel (fedmx_train_hw.hip: W4's gradient and Adam on a
+    second wave per SIMD, validation over 8 waves) performs the same per-element
+    operations as the 4-wave compact kernel: identical parameters, optimizer
+    state, snapshots and early-stop decisions; only the fp64 loss sums are
+    grouped differently."""
+    _, a = _setup_pair(seed=13)
+    _, b = _setup_pair(seed=13)
+    anchor = a.store.params + 0.01 * torch.randn(a.store.params.shape, generator=torch.Generator().manual_seed(7),
+                                                 device="cpu").to(DEV)
+    anchor = canonical_to_padded(padded_to_canonical(anchor.cpu())).to(DEV)
+    a.store.anchor.copy_(anchor)
+    b.store.anchor.copy_(anchor)
+    hp = TrainHParams(epochs=epochs, batch_size=batch, lr=1e-3, shrink_lambda=lam, fedprox_mu=mu, patience=patience)
+    for _ in range(2):   # second launch: persistent Adam state and step counts
+        ta, ea, ba = _hip.train(a.store, [0, 1], hp, a.dims, helper=True)
+        tb, eb, bb = _hip.train(b.store, [0, 1], hp, b.dims, helper=False)
+        torch.cuda.synchronize()
+        _hip.runtime(DEV).sync()
+        assert list(ea) == list(eb) and list(ba) == list(bb)
+        np.testing.assert_allclose(np.array(ta), np.array(tb), rtol=1e-9, atol=1e-12)
+        for name in ("params", "best", "adam_m", "adam_v", "adam_step"):
+            assert torch.equal(getattr(a.store, name), getattr(b.store, name)), name
+
+
 def test_train_kernel_single_step_tight():
     # one Adam step from identical state: errors are pure fp32 rounding
     ref, hip = _setup_pair(n_train=(12,), n_valid=(12,), seed=3)
