@@ -116,7 +116,8 @@ def _template(dims: ModelDims) -> "_CptTemplate":
     if tpl is None:
         tpl = _TEMPLATES[dims] = _CptTemplate(dims)
     if not hasattr(tpl, "np_blob"):
-        tpl.np_blob = np.frombuffer(bytes(tpl.blob), dtype=np.uint8)
+        tpl.blob_bytes = bytes(tpl.blob)
+        tpl.np_blob = np.frombuffer(tpl.blob_bytes, dtype=np.uint8)
         tpl.np_regions = np.ascontiguousarray(np.asarray(tpl.regions, dtype=np.int64).reshape(-1, 3))
     return tpl
 
@@ -148,9 +149,11 @@ def write_round_artifacts(files, save_dirs: Sequence[str], snap: np.ndarray, row
         return
     tpl = _template(dims)
     cpt_paths, trk_paths = zip(*[_artifact_paths(d) for d in save_dirs])
-    fd_cpt = np.asarray([files.open_overwrite(p, 2 * n) for p in cpt_paths], dtype=np.int32)
+    # model.cpt: fixed-size files kept mapped (template bytes written once);
+    # tracking pickles: cached descriptors
+    cpt_dst = np.asarray([files.mapped(p, tpl.blob_bytes) if improved[j] else 0
+                          for j, p in enumerate(cpt_paths)], dtype=np.int64)
     fd_trk = np.asarray([files.open_overwrite(p, 2 * n) for p in trk_paths], dtype=np.int32)
-    size_cpt = np.asarray([files.size_of(p) for p in cpt_paths], dtype=np.int64)
     size_trk = np.asarray([files.size_of(p) for p in trk_paths], dtype=np.int64)
     lens = np.asarray([len(t) for t in tracking], dtype=np.int32)
     trk = np.zeros((n, max(1, int(lens.max(initial=0))), 2), dtype=np.float64)
@@ -158,14 +161,13 @@ def write_round_artifacts(files, save_dirs: Sequence[str], snap: np.ndarray, row
         if len(t):
             trk[j, :len(t)] = np.asarray(t, dtype=np.float64).reshape(-1, 2)
     if n_threads <= 0:
-        n_threads = max(1, min(4, n // 8))
+        n_threads = 1   # page-cache copies + small pwrites: threads measured no faster
     snap = np.ascontiguousarray(snap, dtype=np.float32)
     status = _host.write_artifacts(snap, np.ascontiguousarray(canon_idx, dtype=np.int32), tpl.np_blob,
                                    tpl.np_regions, np.asarray(rows, dtype=np.int32),
-                                   np.asarray(improved, dtype=np.int32), fd_cpt, fd_trk, size_cpt, size_trk,
+                                   np.asarray(improved, dtype=np.int32), cpt_dst, fd_trk, size_trk,
                                    trk, lens, n_threads)
     for j in range(n):
-        files.set_size(cpt_paths[j], size_cpt[j])
         files.set_size(trk_paths[j], size_trk[j])
         if status[j] == -1:      # too many epochs for the native pickler
             if improved[j]:

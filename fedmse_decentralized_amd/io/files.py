@@ -23,6 +23,7 @@ class ArtifactFiles:
         self.max_open = max_open
         self._fds: "OrderedDict[Tuple[str, str], int]" = OrderedDict()
         self._size: Dict[str, int] = {}
+        self._maps: Dict[str, Tuple[int, int]] = {}   # path -> (address, size) of mapped files
 
     def _fd(self, path: str, mode: str) -> int:
         key = (path, mode)
@@ -34,7 +35,7 @@ class ArtifactFiles:
         if d:
             os.makedirs(d, exist_ok=True)
         if mode == "w":
-            fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
+            fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o644)   # read access: shared mappings
             self._size[path] = os.fstat(fd).st_size
         else:
             fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644)
@@ -64,6 +65,28 @@ class ArtifactFiles:
             self.max_open = reserve + 16
         return self._fd(path, "w")
 
+    def mapped(self, path: str, content: bytes) -> int:
+        """Address of a shared writable mapping of ``path`` (a fixed-size file
+        rewritten every round, e.g. model.cpt).  The first call for a path
+        resizes the file to ``len(content)`` and writes ``content`` through the
+        mapping; later calls return the same mapping, whose bytes the caller
+        patches in place."""
+        m = self._maps.get(path)
+        if m is not None and m[1] == len(content):
+            return m[0]
+        from ..ops import _host
+
+        if m is not None:
+            _host.unmap_file(*m)
+        fd = self._fd(path, "w")
+        addr = _host.map_file(fd, len(content))
+        import ctypes
+
+        ctypes.memmove(addr, content, len(content))
+        self._maps[path] = (addr, len(content))
+        self._size[path] = len(content)
+        return addr
+
     def size_of(self, path: str) -> int:
         return self._size.get(path, 0)
 
@@ -78,6 +101,12 @@ class ArtifactFiles:
             off += os.write(fd, view[off:])
 
     def close(self) -> None:
+        if self._maps:
+            from ..ops import _host
+
+            for addr, size in self._maps.values():
+                _host.unmap_file(addr, size)
+            self._maps.clear()
         for fd in self._fds.values():
             os.close(fd)
         self._fds.clear()

@@ -31,9 +31,13 @@ def lib():
             L.fedmx_pickle_tracking.restype = ctypes.c_int64
             L.fedmx_write_artifacts.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                                                 ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
-                                                ctypes.c_int32] + [ctypes.c_void_p] * 8 + [ctypes.c_int32,
+                                                ctypes.c_int32] + [ctypes.c_void_p] * 7 + [ctypes.c_int32,
                                                                                           ctypes.c_void_p,
                                                                                           ctypes.c_int32]
+            L.fedmx_map_file.argtypes = [ctypes.c_int32, ctypes.c_int64]
+            L.fedmx_map_file.restype = ctypes.c_void_p
+            L.fedmx_unmap_file.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+            L.fedmx_unmap_file.restype = ctypes.c_int32
             L.fedmx_write_artifacts.restype = ctypes.c_int32
             _lib = L
     return _lib
@@ -74,13 +78,27 @@ def pickle_tracking(tracking) -> bytes:
     return out[:n].tobytes()
 
 
+def map_file(fd: int, size: int) -> int:
+    """Shared writable mapping of ``fd`` resized to ``size`` bytes (address)."""
+    p = lib().fedmx_map_file(fd, size)
+    if not p:
+        raise OSError(f"cannot map artefact file (fd {fd}, {size} bytes)")
+    return int(p)
+
+
+def unmap_file(addr: int, size: int) -> None:
+    lib().fedmx_unmap_file(addr, size)
+
+
 def write_artifacts(snap: np.ndarray, canon_idx: np.ndarray, tpl: np.ndarray, regions: np.ndarray,
-                    rows: np.ndarray, improved: np.ndarray, fd_cpt: np.ndarray, fd_trk: np.ndarray,
-                    size_cpt: np.ndarray, size_trk: np.ndarray, trk: np.ndarray, trk_len: np.ndarray,
+                    rows: np.ndarray, improved: np.ndarray, cpt_dst: np.ndarray, fd_trk: np.ndarray,
+                    size_trk: np.ndarray, trk: np.ndarray, trk_len: np.ndarray,
                     n_threads: int = 1) -> np.ndarray:
     """One round's model.cpt + training_tracking.pkl files (see
-    csrc/host/fedmx_artifacts.cpp).  ``size_cpt`` / ``size_trk`` are updated in
-    place; returns the per-job status (0 = written)."""
+    csrc/host/fedmx_artifacts.cpp): parameters patched into the mapped
+    model.cpt files at ``cpt_dst`` (addresses), tracking pickles written into
+    ``fd_trk``.  ``size_trk`` is updated in place; returns the per-job status
+    (0 = written)."""
     n = int(rows.shape[0])
     status = np.zeros(n, dtype=np.int32)
     assert snap.dtype == np.float32 and snap.flags.c_contiguous and trk.dtype == np.float64
@@ -88,7 +106,7 @@ def write_artifacts(snap: np.ndarray, canon_idx: np.ndarray, tpl: np.ndarray, re
     lib().fedmx_write_artifacts(
         snap.ctypes.data, snap.shape[1], canon_idx.ctypes.data, canon_idx.shape[0],
         tpl.ctypes.data, tpl.shape[0], regions.ctypes.data, regions.shape[0], n,
-        rows.ctypes.data, improved.ctypes.data, fd_cpt.ctypes.data, fd_trk.ctypes.data,
-        size_cpt.ctypes.data, size_trk.ctypes.data, trk.ctypes.data, trk_len.ctypes.data, trk.shape[1],
+        rows.ctypes.data, improved.ctypes.data, cpt_dst.ctypes.data, fd_trk.ctypes.data,
+        size_trk.ctypes.data, trk.ctypes.data, trk_len.ctypes.data, trk.shape[1],
         status.ctypes.data, n_threads)
     return status

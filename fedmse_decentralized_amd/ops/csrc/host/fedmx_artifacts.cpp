@@ -13,8 +13,10 @@
 //   * model.cpt: the byte template of the legacy format (produced once by
 //     torch.save itself, io/checkpoint.py:_CptTemplate) with the canonical
 //     parameters gathered from the padded host snapshot row and patched into
-//     the storage regions; written with one pwrite at offset 0 into an
-//     already-open descriptor.
+//     the storage regions.  The file has a fixed size, so it stays mapped
+//     (MAP_SHARED, fedmx_map_file): the template bytes are written once when
+//     the mapping is made and a round only copies the 27 KB of parameters
+//     into the page cache — no system call per file and round.
 //   * training_tracking.pkl: the exact bytes pickle.dumps(list_of_tuples,
 //     protocol=4) produces (PROTO 4, FRAME when the body is >= 4 bytes,
 //     EMPTY_LIST MEMOIZE, MARK ... APPENDS (or APPEND for one element),
@@ -30,6 +32,7 @@
 #include <cerrno>
 #include <cstdint>
 #include <cstring>
+#include <sys/mman.h>
 #include <thread>
 #include <unistd.h>
 #include <vector>
@@ -110,37 +113,51 @@ int64_t fedmx_pickle_tracking(const double* t, int32_t n, uint8_t* out, int64_t 
   return static_cast<int64_t>(b.size());
 }
 
+// Shared writable mapping of an open file, resized to exactly `size` bytes
+// (nullptr on failure).
+void* fedmx_map_file(int32_t fd, int64_t size) {
+  if (size <= 0 || ftruncate(fd, static_cast<off_t>(size)) != 0) return nullptr;
+  void* p = mmap(nullptr, static_cast<size_t>(size), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  return p == MAP_FAILED ? nullptr : p;
+}
+
+int32_t fedmx_unmap_file(void* p, int64_t size) {
+  return munmap(p, static_cast<size_t>(size)) == 0 ? 0 : -errno;
+}
+
 // One round's artefacts for n_jobs clients.
 //   snap [*, snap_stride] f32 host snapshot; canon_idx[n_canon] gathers the
 //   canonical parameter vector out of a padded row; tpl/regions: the legacy
 //   model.cpt template and its (byte pos, count, canonical offset) triples.
-//   Job j: snapshot row rows[j]; model.cpt into fd_cpt[j] when improved[j];
+//   Job j: snapshot row rows[j]; when improved[j], the parameters are patched
+//   into the mapped model.cpt at cpt_dst[j] (template bytes already there);
 //   tracking trk[j*trk_stride*2 ...] of trk_len[j] epochs into fd_trk[j].
-//   size_cpt / size_trk: current file sizes (in/out).
+//   size_trk: current tracking file sizes (in/out).
 // Returns 0, or the first negative errno / -1 (tracking too long) per job in
 // status[j] and the count of failed jobs as the (negative) return value.
 int32_t fedmx_write_artifacts(const float* snap, int64_t snap_stride, const int32_t* canon_idx, int32_t n_canon,
                               const uint8_t* tpl, int64_t tpl_len, const int64_t* regions, int32_t n_regions,
-                              int32_t n_jobs, const int32_t* rows, const int32_t* improved, const int32_t* fd_cpt,
-                              const int32_t* fd_trk, int64_t* size_cpt, int64_t* size_trk, const double* trk,
+                              int32_t n_jobs, const int32_t* rows, const int32_t* improved, const int64_t* cpt_dst,
+                              const int32_t* fd_trk, int64_t* size_trk, const double* trk,
                               const int32_t* trk_len, int32_t trk_stride, int32_t* status, int32_t n_threads) {
   if (n_jobs <= 0) return 0;
   if (n_threads < 1) n_threads = 1;
   if (n_threads > n_jobs) n_threads = n_jobs;
+  (void)tpl;
+  (void)tpl_len;
   auto work = [&](int j0, int j1) {
-    std::vector<uint8_t> buf(tpl, tpl + tpl_len);
     std::vector<float> canon(static_cast<size_t>(n_canon));
     std::vector<uint8_t> pk;
     for (int j = j0; j < j1; ++j) {
       int st = 0;
       if (improved[j]) {
+        uint8_t* dst = reinterpret_cast<uint8_t*>(cpt_dst[j]);
         const float* row = snap + static_cast<int64_t>(rows[j]) * snap_stride;
         for (int i = 0; i < n_canon; ++i) canon[i] = row[canon_idx[i]];
         for (int r = 0; r < n_regions; ++r) {
           const int64_t pos = regions[3 * r], cnt = regions[3 * r + 1], off = regions[3 * r + 2];
-          std::memcpy(buf.data() + pos, canon.data() + off, static_cast<size_t>(cnt) * 4);
+          std::memcpy(dst + pos, canon.data() + off, static_cast<size_t>(cnt) * 4);
         }
-        st = write_all(fd_cpt[j], buf.data(), buf.size(), &size_cpt[j]);
       }
       if (st == 0) {
         if (!pickle_tracking(trk + static_cast<int64_t>(j) * trk_stride * 2, trk_len[j], pk))
