@@ -75,3 +75,90 @@ def federation_heterogeneity(proportions: np.ndarray) -> float:
         return 0.0
     d = [js_distance(proportions[i], proportions[j]) for i in range(n) for j in range(i + 1, n)]
     return float(np.mean(d))
+
+
+# -- the notebook's other preparation steps ------------------------------------
+
+def subsample_rows(n_rows: int, fraction: float, rng: np.random.Generator) -> np.ndarray:
+    """Row indices of a per-device random subsample of ``int(fraction * n)``
+    rows without replacement — the notebook keeps 5 % of every N-BaIoT
+    device's benign rows and 0.5 % of its attack rows
+    (`Data-Examination.ipynb:661`, `:670`)."""
+    k = int(fraction * n_rows)
+    return np.sort(rng.choice(n_rows, size=k, replace=False)) if k > 0 else np.zeros(0, dtype=np.int64)
+
+
+def holdout_split(n_rows: int, fraction: float, rng: np.random.Generator):
+    """(held-out, remaining) row indices: the notebook holds out
+    ``int(0.4 * n)`` benign rows as the cross-device ``test_normal`` pool
+    before federating the rest (`Data-Examination.ipynb:1271`)."""
+    held = np.sort(rng.choice(n_rows, size=int(fraction * n_rows), replace=False))
+    rest = np.setdiff1d(np.arange(n_rows), held, assume_unique=True)
+    return held, rest
+
+
+def split_by_balancedness(labels: np.ndarray, n_clients: int, classes_per_client: int, balancedness: float,
+                          rng: np.random.Generator, shuffle: bool = True) -> List[np.ndarray]:
+    """The notebook's hand-rolled ``split_data`` (`Data-Examination.ipynb:1290`).
+
+    Client sizes: equal when ``balancedness >= 1``; otherwise geometric
+    (``balancedness ** i``, normalised, mixed 10 % uniform / 90 % geometric,
+    floored, smallest first).  Each client starts at a random class and takes
+    up to ``size // classes_per_client`` rows per class, cycling through the
+    classes until its budget is spent.  Returns each client's row indices (in
+    take order).  Unlike the notebook, a budget that the remaining rows cannot
+    cover ends the client's loop instead of spinning forever.
+    """
+    labels = np.asarray(labels, dtype=np.int64)
+    n = labels.shape[0]
+    n_labels = int(labels.max()) + 1 if n else 0
+    if balancedness >= 1.0:
+        per_client = [n // n_clients] * n_clients
+        per_class = [per_client[0] // classes_per_client] * n_clients
+    else:
+        fr = balancedness ** np.linspace(0, n_clients - 1, n_clients)
+        fr = fr / fr.sum()
+        fr = 0.1 / n_clients + (1 - 0.1) * fr
+        per_client = [int(np.floor(f * n)) for f in fr][::-1]
+        per_class = [max(1, nd // classes_per_client) for nd in per_client]
+    if sum(per_client) > n:
+        raise ValueError("impossible split: the client budgets exceed the data")
+    pools = [list(np.flatnonzero(labels == c)) for c in range(n_labels)]
+    if shuffle:
+        for p in pools:
+            rng.shuffle(p)
+    out = []
+    for i in range(n_clients):
+        idx: List[int] = []
+        budget = per_client[i]
+        c = int(rng.integers(n_labels))
+        while budget > 0 and any(pools):
+            take = min(per_class[i], len(pools[c]), budget)
+            idx += pools[c][:take]
+            pools[c] = pools[c][take:]
+            budget -= take
+            c = (c + 1) % n_labels
+        out.append(np.asarray(idx, dtype=np.int64))
+    return out
+
+
+def split_fixed_label_percentage(labels: np.ndarray, label_distribution, label_percentage: float = 0.1
+                                 ) -> List[np.ndarray]:
+    """The notebook's ``split_data_with_fixed_label_percentage``
+    (`Data-Examination.ipynb:2226`): client k receives, for each label in
+    ``label_distribution[k]``, the first ``floor(count(label) * pct)`` rows of
+    that label still unassigned (counts taken over the whole input)."""
+    labels = np.asarray(labels)
+    uniq, cnt = np.unique(labels, return_counts=True)
+    count = dict(zip(uniq.tolist(), cnt.tolist()))
+    taken = np.zeros(labels.shape[0], dtype=bool)
+    out = []
+    for client_labels in label_distribution:
+        parts = []
+        for lab in client_labels:
+            k = int(np.floor(count.get(lab, 0) * label_percentage))
+            avail = np.flatnonzero((labels == lab) & ~taken)[:k]
+            taken[avail] = True
+            parts.append(avail)
+        out.append(np.concatenate(parts) if parts else np.zeros(0, dtype=np.int64))
+    return out

@@ -36,7 +36,7 @@ per round in both paths.
 from __future__ import annotations
 
 import logging
-import threading
+import weakref
 from collections import deque
 from typing import Dict, List, Optional
 
@@ -140,9 +140,12 @@ class DeviceRound:
         C = st.best.shape[0]
         self.snap_views = [torch.from_numpy(self.snap_buf.view(i * numel * 4, np.float32, numel).reshape(C, -1))
                            for i in range(self.n_snap)]
-        self.snap_free = [threading.Event() for _ in range(self.n_snap)]
-        for e in self.snap_free:
-            e.set()
+        # native checkpoint writer ticket of the job reading each slot (0: free)
+        self.snap_ticket = [0] * self.n_snap
+        self.ckpt = fed.writer.native_ckpt(fed.dims) if fed.cfg.save_checkpoints and fed.local else None
+        if self.ckpt is not None:
+            # queued writes read snap_buf: drain them before it can be freed
+            weakref.finalize(self, self.ckpt.wait, 0)
         self.snap_i = 0
         self.agg_counts = torch.zeros(N, dtype=i32, device=dev)
         self.weights = torch.zeros(max(N, 1), dtype=f32, device=dev)
@@ -351,8 +354,9 @@ class DeviceRound:
                 si = self.snap_i
                 self.snap_i = (si + 1) % self.n_snap
                 with tel.phase("wait_writer"):   # artefact writer backlog (host-bound indicator)
-                    self.snap_free[si].wait()
-                self.snap_free[si].clear()
+                    if self.snap_ticket[si]:
+                        self.ckpt.wait(self.snap_ticket[si])
+                        self.snap_ticket[si] = 0
                 nd = st.best.numel() // 2
                 _hip.copy2_f64(self.snap_buf.dev_ptr + si * st.best.numel() * 4, best_stage.data_ptr(), nd,
                                0, 0, 0, dev)
@@ -421,8 +425,13 @@ class DeviceRound:
                         log.info(f"[Client {c}] Epoch {e + 1} - Training loss: {tl} - Validating loss: {vl}")
             if cfg.save_checkpoints:
                 si = rec["snap_slot"]
-                fed._submit_checkpoints(res, rec["local_sel"], self.snap_views[si], None)
-                fed.writer.submit(self.snap_free[si].set)
+                # the side stream's event (synchronised above) covers the slot's
+                # snapshot copy: the native writer may read it right away
+                sel = rec["local_sel"]
+                self.snap_ticket[si] = self.ckpt.submit(
+                    [fed.save_dirs[c] for c in sel], self.snap_views[si].numpy(), [self._loc(c) for c in sel],
+                    [bool(res.best_epoch[i] >= 0) for i in range(len(sel))],
+                    [list(res.tracking[i]) for i in range(len(sel))])
         verification = []
         if aggregator is not None:
             self.host_agg_counts[aggregator] += 1

@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import os
 import pickle
+import time
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -123,6 +124,8 @@ def _template(dims: ModelDims) -> "_CptTemplate":
 
 
 _PATHS: Dict[str, Tuple[str, str]] = {}
+# FEDMX_WRITER_STATS=1: seconds spent preparing / inside the native writer
+WRITE_STATS = {} if os.environ.get("FEDMX_WRITER_STATS") == "1" else None
 
 
 def _artifact_paths(save_dir: str) -> Tuple[str, str]:
@@ -147,6 +150,8 @@ def write_round_artifacts(files, save_dirs: Sequence[str], snap: np.ndarray, row
     n = len(save_dirs)
     if n == 0:
         return
+    t0 = time.perf_counter() if WRITE_STATS is not None else 0.0
+    c0 = time.thread_time() if WRITE_STATS is not None else 0.0
     tpl = _template(dims)
     cpt_paths, trk_paths = zip(*[_artifact_paths(d) for d in save_dirs])
     # model.cpt: fixed-size files kept mapped (template bytes written once);
@@ -163,10 +168,18 @@ def write_round_artifacts(files, save_dirs: Sequence[str], snap: np.ndarray, row
     if n_threads <= 0:
         n_threads = 1   # page-cache copies + small pwrites: threads measured no faster
     snap = np.ascontiguousarray(snap, dtype=np.float32)
+    t1 = time.perf_counter() if WRITE_STATS is not None else 0.0
+    c1 = time.thread_time() if WRITE_STATS is not None else 0.0
     status = _host.write_artifacts(snap, np.ascontiguousarray(canon_idx, dtype=np.int32), tpl.np_blob,
                                    tpl.np_regions, np.asarray(rows, dtype=np.int32),
                                    np.asarray(improved, dtype=np.int32), cpt_dst, fd_trk, size_trk,
                                    trk, lens, n_threads)
+    if WRITE_STATS is not None:
+        t2 = time.perf_counter()
+        WRITE_STATS["prep"] = WRITE_STATS.get("prep", 0.0) + (t1 - t0)
+        WRITE_STATS["native"] = WRITE_STATS.get("native", 0.0) + (t2 - t1)
+        WRITE_STATS["calls"] = WRITE_STATS.get("calls", 0) + 1
+        WRITE_STATS["prep_cpu"] = WRITE_STATS.get("prep_cpu", 0.0) + (c1 - c0)
     for j in range(n):
         files.set_size(trk_paths[j], size_trk[j])
         if status[j] == -1:      # too many epochs for the native pickler

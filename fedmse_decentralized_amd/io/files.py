@@ -83,6 +83,8 @@ class ArtifactFiles:
         import ctypes
 
         ctypes.memmove(addr, content, len(content))
+        # the mapping keeps the file referenced: release the descriptor
+        os.close(self._fds.pop((path, "w")))
         self._maps[path] = (addr, len(content))
         self._size[path] = len(content)
         return addr

@@ -1,0 +1,97 @@
+"""Native asynchronous checkpoint writer (``ops/csrc/host/fedmx_artifacts.cpp``).
+
+Each round's ``model.cpt`` + ``training_tracking.pkl`` files of the trained
+clients (`src/Trainer/client_trainer.py:337-358`) are written by a C++ thread:
+``submit`` (main thread) maps / opens the files, copies the job's small arrays
+and returns a ticket at once; the C++ thread patches the parameters into the
+mapped ``model.cpt`` files and writes the tracking pickles without touching
+Python, so it never waits for the GIL; ``wait(ticket)`` blocks (GIL released)
+until that job is on disk — the snapshot slot it read may then be reused.
+
+The device-resident round protocol (``engine/device_round.py``) uses it: its
+snapshots live in a mapped host ring that the GPU fills and the writer reads.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence, Tuple
+
+import numpy as np
+
+from ..models.layout import DEFAULT_DIMS, ModelDims, padded_index
+from . import checkpoint as ckpt
+from .files import ArtifactFiles
+
+_MAX_NATIVE_EPOCHS = 1000   # the native pickler's single-batch limit
+
+
+class NativeCheckpointWriter:
+    def __init__(self, dims: ModelDims = DEFAULT_DIMS):
+        from ..ops import _host
+
+        self._lib = _host.lib()
+        self.dims = dims
+        self.tpl = ckpt._template(dims)
+        self.cidx = np.ascontiguousarray(padded_index(dims)[0].numpy(), dtype=np.int32)
+        # owned by the submitting (main) thread; never evicts descriptors a
+        # queued job may still use
+        self.files = ArtifactFiles(max_open=1 << 30)
+        self.h = self._lib.fedmx_writer_create(self.cidx.ctypes.data, self.cidx.shape[0],
+                                               self.tpl.np_regions.ctypes.data, self.tpl.np_regions.shape[0])
+        self.last = 0
+
+    def submit(self, save_dirs: Sequence[str], snap: np.ndarray, rows: Sequence[int], improved: Sequence[bool],
+               tracking: Sequence[Sequence[Tuple[float, float]]]) -> int:
+        """Queue one round's files; ``snap`` (float32 [rows, P_PAD]) must stay
+        valid until ``wait`` of the returned ticket."""
+        n = len(save_dirs)
+        if n == 0:
+            return self.last
+        if any(len(t) > _MAX_NATIVE_EPOCHS for t in tracking):
+            self.flush()
+            ckpt.write_round_artifacts(self.files, save_dirs, snap, rows, improved, tracking, self.cidx, self.dims)
+            return self.last
+        blob = self.tpl.blob_bytes
+        cpt_dst = np.zeros(n, dtype=np.int64)
+        fd_trk = np.empty(n, dtype=np.int32)
+        for j, d in enumerate(save_dirs):
+            pc, pt = ckpt._artifact_paths(d)
+            if improved[j]:
+                cpt_dst[j] = self.files.mapped(pc, blob)
+            fd_trk[j] = self.files.open_overwrite(pt)
+        lens = np.asarray([len(t) for t in tracking], dtype=np.int32)
+        width = max(1, int(lens.max(initial=0)))
+        trk = np.zeros((n, width, 2), dtype=np.float64)
+        for j, t in enumerate(tracking):
+            if len(t):
+                trk[j, :len(t)] = np.asarray(t, dtype=np.float64).reshape(-1, 2)
+        snap = np.asarray(snap)
+        assert snap.dtype == np.float32 and snap.flags.c_contiguous
+        rows_a = np.asarray(rows, dtype=np.int32)
+        imp_a = np.asarray(improved, dtype=np.int32)
+        self.last = int(self._lib.fedmx_writer_submit(
+            self.h, snap.ctypes.data, snap.shape[1], n, rows_a.ctypes.data, imp_a.ctypes.data, cpt_dst.ctypes.data,
+            fd_trk.ctypes.data, trk.ctypes.data, lens.ctypes.data, width))
+        return self.last
+
+    def wait(self, ticket: int) -> None:
+        rc = self._lib.fedmx_writer_wait(self.h, ticket)
+        if rc:
+            raise OSError(-rc if rc < 0 else rc, "native checkpoint writer failed")
+
+    def flush(self) -> None:
+        """Every queued job written; cached descriptors / mappings released."""
+        self.wait(0)
+        self.files.close()
+
+    def close(self) -> None:
+        if self.h:
+            self.flush()
+            self._lib.fedmx_writer_destroy(ctypes.c_void_p(self.h))
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -30,9 +30,13 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <thread>
 #include <unistd.h>
 #include <vector>
@@ -182,6 +186,137 @@ int32_t fedmx_write_artifacts(const float* snap, int64_t snap_stride, const int3
   int32_t bad = 0;
   for (int j = 0; j < n_jobs; ++j) bad += status[j] != 0;
   return -bad;
+}
+
+// ---------------------------------------------------------------------------
+// Asynchronous native writer thread.  The device-resident round protocol
+// collects round r's results while the GPU already runs r+1 / r+2; handing
+// the checkpoint writes to a Python thread made them wait for the GIL behind
+// the enqueueing main thread (64 clients: ~5 ms of GIL waits per round for
+// ~0.2 ms of work).  Here a submit copies the job's small arrays and returns
+// a ticket; a C++ thread patches the mapped model.cpt files and writes the
+// tracking pickles; fedmx_writer_wait(ticket) blocks (GIL released by
+// ctypes) until that job is done — the snapshot slot it reads may then be
+// reused.
+namespace {
+
+struct WJob {
+  const float* snap;
+  int64_t stride;
+  std::vector<int32_t> rows, improved, fd_trk, trk_len;
+  std::vector<int64_t> cpt_dst;
+  std::vector<double> trk;
+  int32_t trk_stride;
+  int64_t ticket;
+};
+
+struct Writer {
+  std::vector<int32_t> canon_idx;
+  std::vector<int64_t> regions;
+  std::mutex mu;
+  std::condition_variable cv_job, cv_done;
+  std::deque<WJob> q;
+  int64_t next_ticket = 0, done_ticket = 0;
+  int32_t first_error = 0;
+  bool stop = false;
+  std::thread th;
+
+  void run() {
+    std::vector<float> canon(canon_idx.size());
+    std::vector<uint8_t> pk;
+    for (;;) {
+      WJob job;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_job.wait(lk, [&] { return stop || !q.empty(); });
+        if (q.empty()) return;
+        job = std::move(q.front());
+        q.pop_front();
+      }
+      int32_t err = 0;
+      const int n = static_cast<int>(job.rows.size());
+      const int nreg = static_cast<int>(regions.size() / 3);
+      for (int j = 0; j < n; ++j) {
+        if (job.improved[j]) {
+          uint8_t* dst = reinterpret_cast<uint8_t*>(job.cpt_dst[j]);
+          const float* row = job.snap + static_cast<int64_t>(job.rows[j]) * job.stride;
+          for (size_t i = 0; i < canon.size(); ++i) canon[i] = row[canon_idx[i]];
+          for (int r = 0; r < nreg; ++r)
+            std::memcpy(dst + regions[3 * r], canon.data() + regions[3 * r + 2],
+                        static_cast<size_t>(regions[3 * r + 1]) * 4);
+        }
+        if (!pickle_tracking(job.trk.data() + static_cast<int64_t>(j) * job.trk_stride * 2, job.trk_len[j], pk)) {
+          if (!err) err = -1;
+          continue;
+        }
+        struct stat st;
+        int64_t old = fstat(job.fd_trk[j], &st) == 0 ? static_cast<int64_t>(st.st_size) : 0;
+        const int rc = write_all(job.fd_trk[j], pk.data(), pk.size(), &old);
+        if (rc && !err) err = rc;
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        if (err && !first_error) first_error = err;
+        done_ticket = job.ticket;
+      }
+      cv_done.notify_all();
+    }
+  }
+};
+
+}  // namespace
+
+void* fedmx_writer_create(const int32_t* canon_idx, int32_t n_canon, const int64_t* regions, int32_t n_regions) {
+  Writer* w = new Writer();
+  w->canon_idx.assign(canon_idx, canon_idx + n_canon);
+  w->regions.assign(regions, regions + 3 * static_cast<int64_t>(n_regions));
+  w->th = std::thread([w] { w->run(); });
+  return w;
+}
+
+// Queue one round's checkpoint job; returns its ticket (> 0).
+int64_t fedmx_writer_submit(void* handle, const float* snap, int64_t stride, int32_t n, const int32_t* rows,
+                            const int32_t* improved, const int64_t* cpt_dst, const int32_t* fd_trk, const double* trk,
+                            const int32_t* trk_len, int32_t trk_stride) {
+  Writer* w = static_cast<Writer*>(handle);
+  WJob job;
+  job.snap = snap;
+  job.stride = stride;
+  job.rows.assign(rows, rows + n);
+  job.improved.assign(improved, improved + n);
+  job.cpt_dst.assign(cpt_dst, cpt_dst + n);
+  job.fd_trk.assign(fd_trk, fd_trk + n);
+  job.trk_len.assign(trk_len, trk_len + n);
+  job.trk.assign(trk, trk + static_cast<int64_t>(n) * trk_stride * 2);
+  job.trk_stride = trk_stride;
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    job.ticket = ++w->next_ticket;
+    w->q.push_back(std::move(job));
+  }
+  w->cv_job.notify_one();
+  return w->next_ticket;
+}
+
+// Block until job `ticket` (and every earlier one) is written; ticket <= 0:
+// every submitted job.  Returns the first write error seen so far (0: none).
+int32_t fedmx_writer_wait(void* handle, int64_t ticket) {
+  Writer* w = static_cast<Writer*>(handle);
+  std::unique_lock<std::mutex> lk(w->mu);
+  const int64_t t = ticket > 0 ? ticket : w->next_ticket;
+  w->cv_done.wait(lk, [&] { return w->done_ticket >= t; });
+  return w->first_error;
+}
+
+void fedmx_writer_destroy(void* handle) {
+  Writer* w = static_cast<Writer*>(handle);
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    w->stop = true;
+  }
+  w->cv_job.notify_all();
+  w->th.join();
+  delete w;
 }
 
 }  // extern "C"

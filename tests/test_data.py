@@ -144,3 +144,42 @@ def test_dirichlet_split_and_js():
             assert (lab == cl).sum() >= 10
     assert js_distance([1, 0], [1, 0]) == 0.0
     assert abs(js_distance([1, 0], [0, 1]) - 1.0) < 1e-12
+
+
+def test_notebook_splitters():
+    import numpy as np
+
+    from fedmse_decentralized_amd.data import partition as P
+
+    rng = np.random.default_rng(0)
+    labels = rng.integers(0, 9, size=5000)
+    # equal-size clients, each cycling through its classes
+    parts = P.split_by_balancedness(labels, 10, 3, 1.0, np.random.default_rng(1))
+    assert [len(p) for p in parts] == [500] * 10
+    allidx = np.concatenate(parts)
+    assert len(np.unique(allidx)) == allidx.size          # disjoint
+    # skewed sizes: smallest first, geometric in balancedness
+    parts = P.split_by_balancedness(labels, 10, 3, 0.8, np.random.default_rng(1))
+    sizes = [len(p) for p in parts]
+    assert sizes == sorted(sizes) and sizes[0] < sizes[-1]
+    fr = 0.8 ** np.linspace(0, 9, 10)
+    fr = 0.01 + 0.9 * fr / fr.sum()
+    assert sizes == [int(np.floor(f * 5000)) for f in fr][::-1]
+    # fixed label percentage: floor(count * pct) first unassigned rows per label
+    dist = [[0, 2, 4], [0, 4, 3, 1], [5, 3, 0]]
+    parts = P.split_fixed_label_percentage(labels, dist, 0.1)
+    for k, labs in enumerate(dist):
+        for lab in labs:
+            got = parts[k][labels[parts[k]] == lab]
+            assert len(got) == int(np.floor((labels == lab).sum() * 0.1))
+    assert len(np.unique(np.concatenate(parts))) == sum(len(p) for p in parts)
+    # label 0 appears in three clients: later clients take the next rows
+    z = np.flatnonzero(labels == 0)
+    k0 = int(np.floor(len(z) * 0.1))
+    assert np.array_equal(parts[0][labels[parts[0]] == 0], z[:k0])
+    assert np.array_equal(parts[1][labels[parts[1]] == 0], z[k0:2 * k0])
+    # per-device subsample and the 40 % test_normal holdout
+    s = P.subsample_rows(10000, 0.05, rng)
+    assert s.size == 500 and np.unique(s).size == 500
+    held, rest = P.holdout_split(1000, 0.4, rng)
+    assert held.size == 400 and rest.size == 600 and not set(held) & set(rest)

@@ -93,3 +93,37 @@ def test_native_round_writer_matches_python_writers(tmp_path):
 
     sd = _t.load(os.path.join(nat[0], "model.cpt"), weights_only=True)
     assert list(sd.keys())[0] == "encoder.encoder_network.0.weight"
+
+
+def test_native_async_writer_matches_python_writers(tmp_path):
+    """NativeCheckpointWriter (C++ thread, tickets) leaves the bytes of
+    save_model_cpt_fast / save_tracking; wait(ticket) orders slot reuse."""
+    from fedmse_decentralized_amd.io.native_writer import NativeCheckpointWriter
+    from fedmse_decentralized_amd.models.layout import P_PAD, padded_index
+
+    cidx = padded_index(DEFAULT_DIMS)[0].numpy()
+    rng = np.random.default_rng(5)
+    w = NativeCheckpointWriter(DEFAULT_DIMS)
+    n = 12
+    nat = [str(tmp_path / "nat" / f"c{i}") for i in range(n)]
+    ref = [str(tmp_path / "ref" / f"c{i}") for i in range(n)]
+    slots = [rng.normal(size=(n + 2, P_PAD)).astype(np.float32) for _ in range(2)]
+    tickets = [0, 0]
+    for rnd in range(6):
+        si = rnd % 2
+        if tickets[si]:
+            w.wait(tickets[si])
+        slots[si][:] = rng.normal(size=slots[si].shape).astype(np.float32)
+        rows = rng.permutation(n + 2)[:n]
+        improved = [True] * n if rnd == 0 else [bool(x) for x in rng.integers(0, 2, size=n)]
+        trks = [[(float(a), float(b)) for a, b in rng.normal(size=(int(rng.integers(1, 6)), 2))] for _ in range(n)]
+        for j in range(n):
+            if improved[j]:
+                ckpt.save_model_cpt_fast(ref[j], slots[si][rows[j]][cidx], DEFAULT_DIMS)
+            ckpt.save_tracking(ref[j], trks[j])
+        tickets[si] = w.submit(nat, slots[si], rows, improved, trks)
+    w.flush()
+    for a, b in zip(nat, ref):
+        for name in ("model.cpt", "training_tracking.pkl"):
+            assert open(os.path.join(a, name), "rb").read() == open(os.path.join(b, name), "rb").read()
+    w.close()

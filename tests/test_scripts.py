@@ -61,3 +61,36 @@ def test_bench_stdout_is_one_json_line():
     assert rec["higher_is_better"] is True and rec["value"] > 0
     for k in ("model", "global_batch", "seq_len", "parallelism"):
         assert k in rec["config"], k
+
+
+def test_partition_devices_pipeline(tmp_path):
+    """scripts/partition_devices.py: per-device subsample, 40 % test_normal
+    holdout, Dirichlet split, reference layout readable by the CSV loader."""
+    import numpy as np
+
+    import partition_devices as mod
+    rng = np.random.default_rng(0)
+    raw = tmp_path / "raw"
+    args = []
+    for d in range(3):
+        (raw / f"dev{d}").mkdir(parents=True)
+        hdr = ",".join(f"f{i}" for i in range(115))
+        np.savetxt(raw / f"dev{d}" / "benign_traffic.csv", rng.normal(size=(4000, 115)), delimiter=",",
+                   header=hdr, comments="")
+        np.savetxt(raw / f"dev{d}" / "attack.csv", rng.normal(5, 1, size=(4000, 115)), delimiter=",",
+                   header=hdr, comments="")
+        args += ["--device", f"dev{d}={raw}/dev{d}/benign_traffic.csv:{raw}/dev{d}/attack*.csv"]
+    out = tmp_path / "fed"
+    assert mod.main(args + ["--out", str(out), "--clients", "4", "--min-count", "0", "--abnormal-frac", "0.05"]) == 0
+    cfg = json.load(open(out / "Configuration" / "federated.json"))
+    assert len(cfg["devices_list"]) == 4
+    from fedmse_decentralized_amd.data.csv import load_data
+
+    tot = {"normal": 0, "abnormal": 0, "test_normal": 0}
+    for dev in cfg["devices_list"]:
+        for split in tot:
+            arr = load_data(str(out / "Data" / dev[f"{split}_data_path"]))
+            assert arr.shape[1] == 115
+            tot[split] += arr.shape[0]
+    # 5 % of 3 x 4000 benign = 600 (40 % held out), 5 % of 3 x 4000 attack = 600
+    assert tot == {"normal": 360, "abnormal": 600, "test_normal": 240}
