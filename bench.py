@@ -228,6 +228,7 @@ def _main(argv, real_stdout: int):
         if args.out:
             with open(args.out, "w") as f:
                 f.write(line + "\n")
+    fed.writer.report_stats()   # FEDMX_WRITER_STATS=1: per-job writer times on stderr
     shutdown(comm)
     return 0
 

@@ -103,7 +103,8 @@ class AsyncWriter:
             errs, self.errors = self.errors, []
             raise RuntimeError("artefact writer failed:\n" + "\n".join(errs))
 
-    def close(self):
+    def report_stats(self):
+        """FEDMX_WRITER_STATS=1: per job kind count / total / mean time on stderr."""
         if self.stats:
             print("writer job stats (count, total ms, us/job):", file=sys.stderr)
             for k, (n, tot) in sorted(self.stats.items(), key=lambda kv: -kv[1][1]):
@@ -111,11 +112,14 @@ class AsyncWriter:
             from .checkpoint import WRITE_STATS
             if WRITE_STATS:
                 print(f"  write_round_artifacts: {WRITE_STATS}", file=sys.stderr)
+
+    def close(self):
         if self.enabled and self.t is not None:
             self.flush()
             self.q.put(None)
             self.t.join()
             self.t = None
+            self.enabled = False   # a closed writer runs later jobs inline
         if self.native is not None:
             self.native.close()
             self.native = None

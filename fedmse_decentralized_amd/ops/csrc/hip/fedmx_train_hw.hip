@@ -26,6 +26,13 @@
 // published, loss exchange, snapshot; epilogue write-back.
 #include "fedmx_train_common.h"
 
+// Timing-only ablations of the main waves' step (WRONG numerics, never a
+// production build): 2 = no loss accumulation, 4 = no small-tile gradient /
+// Adam.  (1 = no per-step Adam constants on the mains, -6.3 %, led to the
+// helper-side computation below.)
+#ifndef FEDMX_HW_ABLATE
+#define FEDMX_HW_ABLATE 0
+#endif
 // issue priority of the main waves over their helpers (s_setprio level; 0: equal)
 #ifndef FEDMX_HW_PRIO
 #define FEDMX_HW_PRIO 0
@@ -145,6 +152,9 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   float* const sDZT = sZT + L_T16;       // dZ^T
   float* const sQ4 = sRedDH3 + L_RED + 4 * L_SCR;   // [w][v][t][lane][4]
   double* const sLoss = reinterpret_cast<double*>(sQ4 + L_Q4);  // [8 waves][4]
+  // per-step Adam scalars (helper -> main), double-buffered by step parity:
+  // [neg_step_size, inv_bc2s, bc2s, -]
+  float* const sK = reinterpret_cast<float*>(sLoss + 32);
 
   Lane L;
   L.w1 = sW1 + c * S_W1 + 32 * w + 4 * g;
@@ -445,11 +455,20 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           lds_write4(q4p + (2 * v + t) * 256, f32x4{P4.q4[v][t][0], P4.q4[v][t][1], P4.q4[v][t][2], P4.q4[v][t][3]});
     };
     publish_q4();
+    // The step's Adam scalars (f64 bias corrections: ~6 % of the main waves'
+    // step when they computed them, FEDMX_HW_ABLATE=1) are formed here one
+    // step ahead and handed over through LDS.
+    int js = 0;   // step index within the launch
+    auto publish_k = [&]() {
+      next_constants();
+      if (lane == 0 && w8 == 4)
+        lds_write4(sK + 4 * (js & 1), f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f});
+    };
+    publish_k();   // step 0's
     for (int ep = 0; ep < A.epochs; ++ep) {
       double acc_tr = 0.0;
       // W4 gradient + Adam between barrier #2 of step s and barrier #1 of s+1
       for (int bi = 0; bi < nb; ++bi) {
-        next_constants();
         __syncthreads();   // barrier #1 (main: layer-1 partials)
         __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
         const f32x4 w4a0 = lds_read4(sT0 + tr);
@@ -479,6 +498,8 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         // dH3 A-operand copy; main w reads both after barrier #1 of step s+1
         w4_to_lds(P4, L);
         publish_q4();
+        ++js;
+        publish_k();   // step js's scalars, read by the mains after its barrier #1
       }
       double prox_now = 0.0;
       if (PROX) {
@@ -508,6 +529,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   }
 
   // ============================= main waves =====================================
+  int js = 0;   // step index within the launch (selects the Adam-scalar slot)
   // (FEDMX_HW_PRIO: the chain's wave wins issue arbitration against its helper)
   if (FEDMX_HW_PRIO) __builtin_amdgcn_s_setprio(FEDMX_HW_PRIO);
   MSlab P, M, V, AN;
@@ -556,7 +578,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       const int row_n = (bi + 1) * B;
       const int bc_n = has_next ? min(B, n_tr - row_n) : 0;
       const float inv_bt = 1.0f / (float)bt;
-      next_constants();
       f32x4 G1[2][2], Go = zero4();
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -571,6 +592,14 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         lds_write4(red + (w * 2 + 0) * 256 + lane * 4, l1a);
         lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1b);
         __syncthreads();  // barrier #1
+        {
+          // this step's Adam scalars (helper-published)
+          const f32x4 kk = lds_read4(sK + 4 * (js & 1));
+          K.neg_step_size = kk[0];
+          K.inv_bc2s = kk[1];
+          K.bc2s = kk[2];
+          ++js;
+        }
         // W4(s) rows in the dH3 A-operand layout (helper-published)
 #pragma unroll
         for (int v = 0; v < 2; ++v)
@@ -654,7 +683,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         norm_c = __builtin_amdgcn_sqrtf(nz);
         float contrib = sq * (inv_bt * inv_d);
         if (w == 0 && g == 0 && col_ok) contrib += lam * norm_c * inv_bt;
-        acc_tr += (double)contrib;
+        if (!(FEDMX_HW_ABLATE & 2)) acc_tr += (double)contrib;
       }
       if (has_next) load_chunk(Xtr, row_n, bc_n, nxt);  // prefetch
 
@@ -751,7 +780,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
       wave_sync();
       // ---- owned small tile: w<2 -> dW3 tile = dH3^T Z ; w>=2 -> dW2 tile = dZ^T H1
-      {
+      if (!(FEDMX_HW_ABLATE & 4)) {
         const f32x4 a = lds_read4(w < 2 ? sT2 + tr + 16 * w * S_T : sDZT + tr);
         const f32x4 bz = lds_read4(sZT + tr);
         const f32x4 b = (w < 2) ? bz : ((w == 2) ? h1b[0] : h1b[1]);
@@ -766,9 +795,9 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       // (after an epoch's last batch this works on a stale tile; unused)
       finalize_chunk(nxt);
       l1_partial(nxt, l1a, l1b);
-      adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
+      if (!(FEDMX_HW_ABLATE & 4)) adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
       if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
-      own_to_lds(P, L);   // read by every wave after barrier #1
+      if (!(FEDMX_HW_ABLATE & 4)) own_to_lds(P, L);   // read by every wave after barrier #1
       __builtin_amdgcn_iglp_opt(0);
       cur = nxt;
     }

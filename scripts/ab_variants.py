@@ -31,6 +31,11 @@ VARIANTS = {
     "hwprio1": ["-DFEDMX_HW_PRIO=1"],             # main waves at issue priority 1 over helpers (+0.4%)
     "hwprio3": ["-DFEDMX_HW_PRIO=3"],             # main waves at issue priority 3 (+0.4%)
     "scaled": ["-DFEDMX_ADAM_SCALED=1"],          # scaled-moment Adam, 5 VALU/param (+0.5%)
+    # helper-wave kernel, timing-only ablations of the main waves' step (r2, base
+    # 1.059 ms; per-step Adam constants on the mains: 0.992 ms without -> moved
+    # to the helpers)
+    "hwabl_loss": ["-DFEDMX_HW_ABLATE=2"],        # no loss accumulation          1.044 ms
+    "hwabl_small": ["-DFEDMX_HW_ABLATE=4"],       # no small-tile gradient / Adam 1.024 ms
     # timing-only ablations (wrong numerics): what each optimizer piece costs
     # on the critical path (r2, base 1.095 ms)
     "abl_w4": ["-DFEDMX_ABLATE=1"],               # no dW4 / W4 Adam          0.991 ms (-9.5%)
