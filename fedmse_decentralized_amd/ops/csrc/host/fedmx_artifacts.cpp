@@ -86,7 +86,28 @@ bool pickle_tracking(const double* t, int n, std::vector<uint8_t>& out) {
   return true;
 }
 
+// First content of a new (empty) file through a temporary shared mapping:
+// on the GPU hosts' filesystem the first write(2) into a new file costs
+// ~2.8 ms (block allocation on the caller's thread) while a mapping's dirty
+// pages are allocated by the kernel's writeback (~0.09 ms for a new 28 KB
+// model.cpt, scripts/first_write_probe.py).
+int write_new_mapped(int fd, const uint8_t* p, size_t n) {
+  if (ftruncate(fd, static_cast<off_t>(n)) != 0) return -errno;
+  void* m = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (m == MAP_FAILED) return -errno;
+  std::memcpy(m, p, n);
+  munmap(m, n);
+  return 0;
+}
+
 int write_all(int fd, const uint8_t* p, size_t n, int64_t* size_io) {
+  if (*size_io == 0 && n > 0) {
+    const int rc = write_new_mapped(fd, p, n);
+    if (rc == 0) {
+      *size_io = static_cast<int64_t>(n);
+      return 0;
+    }
+  }
   size_t off = 0;
   while (off < n) {
     const ssize_t w = pwrite(fd, p + off, n - off, static_cast<off_t>(off));

@@ -35,6 +35,9 @@ VARIANTS = {
     # 1.059 ms; per-step Adam constants on the mains: 0.992 ms without -> moved
     # to the helpers)
     "hwabl_loss": ["-DFEDMX_HW_ABLATE=2"],        # no loss accumulation          1.044 ms
+    # (moving the loss share to the helpers measured 1.066 vs 0.966 ms: the helpers'
+    # work between barrier #2 and #1 is on the step's path once it exceeds the
+    # mains'; a per-chunk Adam-scalar table instead of per-step scalars: 0.974 ms)
     "hwabl_small": ["-DFEDMX_HW_ABLATE=4"],       # no small-tile gradient / Adam 1.024 ms
     # timing-only ablations (wrong numerics): what each optimizer piece costs
     # on the critical path (r2, base 1.095 ms)
