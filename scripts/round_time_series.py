@@ -22,6 +22,7 @@ def main(argv=None):
     p.add_argument("--data-kind", default="kitsune")
     p.add_argument("--non-iid", action="store_true")
     p.add_argument("--no-artifacts", action="store_true")
+    p.add_argument("--profile-rounds", type=int, default=0, help="cProfile the first N rounds (stderr)")
     a = p.parse_args(argv)
     from fedmse_decentralized_amd.config import ExperimentConfig
     from fedmse_decentralized_amd.federation import Federation
@@ -34,8 +35,20 @@ def main(argv=None):
                            global_early_stop=False, save_checkpoints=not a.no_artifacts,
                            output_root=tempfile.mkdtemp(prefix="fedmx_ts_"), log_level="WARNING")
     fed = Federation(cfg, "hybrid", "mse_avg", run=0, write_reports=not a.no_artifacts).setup()
+    prof = None
+    if a.profile_rounds:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     ts = [time.perf_counter()]
     for r in range(a.rounds):
+        if prof is not None and r == a.profile_rounds:
+            prof.disable()
+            import pstats
+
+            pstats.Stats(prof, stream=sys.stderr).sort_stats("cumtime").print_stats(25)
+            prof = None
         if r and r % 20 == 0:
             fed.reset_aggregation_counts()
         fed.run_round()
