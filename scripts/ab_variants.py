@@ -35,6 +35,8 @@ VARIANTS = {
     # 1.059 ms; per-step Adam constants on the mains: 0.992 ms without -> moved
     # to the helpers)
     "hwabl_loss": ["-DFEDMX_HW_ABLATE=2"],        # no loss accumulation          1.044 ms
+    # (small tiles read as 16-byte D-layout copies instead of 16 scalar LDS reads:
+    # 0.965 vs 0.966 ms, FedProx 1.089 vs 1.043 -- reverted)
     # (moving the loss share to the helpers measured 1.066 vs 0.966 ms: the helpers'
     # work between barrier #2 and #1 is on the step's path once it exceeds the
     # mains'; a per-chunk Adam-scalar table instead of per-step scalars: 0.974 ms)
