@@ -71,13 +71,21 @@ def test_device_round_matches_host_path(tmp_path, update_type):
     assert torch.equal(fa.engine.store.params, fb.engine.store.params)
     assert torch.equal(fa.engine.store.anchor, fb.engine.store.anchor)
     assert fa.agg_counts == fb.agg_counts
-    # identical report files
+    # identical report files and checkpoint artefacts (device path: the native
+    # writer thread; host path: the Python writer job)
+    n_ckpt = 0
     for root_a, _, files in os.walk(str(tmp_path / "dev")):
         for fn in files:
+            if fn in ("model.cpt", "training_tracking.pkl"):
+                pa = os.path.join(root_a, fn)
+                pb = pa.replace(str(tmp_path / "dev"), str(tmp_path / "host"))
+                assert open(pa, "rb").read() == open(pb, "rb").read(), pa
+                n_ckpt += 1
             if fn.endswith(".json"):
                 pa = os.path.join(root_a, fn)
                 pb = pa.replace(str(tmp_path / "dev"), str(tmp_path / "host"))
                 assert open(pa).read() == open(pb).read(), fn
+    assert n_ckpt >= 2 * 3   # every client trained at least once in 6 rounds of 3 selections
 
 
 def test_device_round_early_stop_and_episode_reset(tmp_path):
