@@ -2,11 +2,14 @@
 
 Each round's ``model.cpt`` + ``training_tracking.pkl`` files of the trained
 clients (`src/Trainer/client_trainer.py:337-358`) are written by a C++ thread:
-``submit`` (main thread) maps / opens the files, copies the job's small arrays
-and returns a ticket at once; the C++ thread patches the parameters into the
-mapped ``model.cpt`` files and writes the tracking pickles without touching
-Python, so it never waits for the GIL; ``wait(ticket)`` blocks (GIL released)
-until that job is on disk — the snapshot slot it read may then be reused.
+``submit`` (main thread) copies the job's small arrays and paths and returns a
+ticket at once, with no system call; the C++ thread opens / creates the files
+(kept open, ``model.cpt`` kept mapped), patches the parameters into the mapped
+``model.cpt`` files and writes the tracking pickles without touching Python,
+so it never waits for the GIL and the main thread never waits for the
+filesystem (file creation on the GPU hosts' filesystem costs ~1 ms each);
+``wait(ticket)`` blocks (GIL released) until that job is on disk — the
+snapshot slot it read may then be reused.
 
 The device-resident round protocol (``engine/device_round.py``) uses it: its
 snapshots live in a mapped host ring that the GPU fills and the writer reads.
@@ -14,6 +17,7 @@ snapshots live in a mapped host ring that the GPU fills and the writer reads.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Sequence, Tuple
 
 import numpy as np
@@ -33,11 +37,11 @@ class NativeCheckpointWriter:
         self.dims = dims
         self.tpl = ckpt._template(dims)
         self.cidx = np.ascontiguousarray(padded_index(dims)[0].numpy(), dtype=np.int32)
-        # owned by the submitting (main) thread; never evicts descriptors a
-        # queued job may still use
-        self.files = ArtifactFiles(max_open=1 << 30)
+        blob = np.frombuffer(self.tpl.blob_bytes, dtype=np.uint8)
         self.h = self._lib.fedmx_writer_create(self.cidx.ctypes.data, self.cidx.shape[0],
-                                               self.tpl.np_regions.ctypes.data, self.tpl.np_regions.shape[0])
+                                               self.tpl.np_regions.ctypes.data, self.tpl.np_regions.shape[0],
+                                               blob.ctypes.data, blob.shape[0])
+        self._paths = {}
         self.last = 0
 
     def submit(self, save_dirs: Sequence[str], snap: np.ndarray, rows: Sequence[int], improved: Sequence[bool],
@@ -49,16 +53,13 @@ class NativeCheckpointWriter:
             return self.last
         if any(len(t) > _MAX_NATIVE_EPOCHS for t in tracking):
             self.flush()
-            ckpt.write_round_artifacts(self.files, save_dirs, snap, rows, improved, tracking, self.cidx, self.dims)
+            files = ArtifactFiles()
+            try:
+                ckpt.write_round_artifacts(files, save_dirs, snap, rows, improved, tracking, self.cidx, self.dims)
+            finally:
+                files.close()
             return self.last
-        blob = self.tpl.blob_bytes
-        cpt_dst = np.zeros(n, dtype=np.int64)
-        fd_trk = np.empty(n, dtype=np.int32)
-        for j, d in enumerate(save_dirs):
-            pc, pt = ckpt._artifact_paths(d)
-            if improved[j]:
-                cpt_dst[j] = self.files.mapped(pc, blob)
-            fd_trk[j] = self.files.open_overwrite(pt)
+        paths = b"".join(self._path_bytes(d) for d in save_dirs)
         lens = np.asarray([len(t) for t in tracking], dtype=np.int32)
         width = max(1, int(lens.max(initial=0)))
         trk = np.zeros((n, width, 2), dtype=np.float64)
@@ -69,10 +70,20 @@ class NativeCheckpointWriter:
         assert snap.dtype == np.float32 and snap.flags.c_contiguous
         rows_a = np.asarray(rows, dtype=np.int32)
         imp_a = np.asarray(improved, dtype=np.int32)
-        self.last = int(self._lib.fedmx_writer_submit(
-            self.h, snap.ctypes.data, snap.shape[1], n, rows_a.ctypes.data, imp_a.ctypes.data, cpt_dst.ctypes.data,
-            fd_trk.ctypes.data, trk.ctypes.data, lens.ctypes.data, width))
-        return self.last
+        t = int(self._lib.fedmx_writer_submit(
+            self.h, snap.ctypes.data, snap.shape[1], n, rows_a.ctypes.data, imp_a.ctypes.data, paths, len(paths),
+            trk.ctypes.data, lens.ctypes.data, width))
+        if t < 0:
+            raise ValueError("native checkpoint writer: malformed path list")
+        self.last = t
+        return t
+
+    def _path_bytes(self, save_dir: str) -> bytes:
+        b = self._paths.get(save_dir)
+        if b is None:
+            pc, pt = ckpt._artifact_paths(save_dir)
+            b = self._paths[save_dir] = os.fsencode(pc) + b"\0" + os.fsencode(pt) + b"\0"
+        return b
 
     def wait(self, ticket: int) -> None:
         rc = self._lib.fedmx_writer_wait(self.h, ticket)
@@ -80,9 +91,11 @@ class NativeCheckpointWriter:
             raise OSError(-rc if rc < 0 else rc, "native checkpoint writer failed")
 
     def flush(self) -> None:
-        """Every queued job written; cached descriptors / mappings released."""
-        self.wait(0)
-        self.files.close()
+        """Every queued job written; the writer thread's descriptors and
+        mappings released."""
+        rc = self._lib.fedmx_writer_flush(self.h)
+        if rc:
+            raise OSError(-rc if rc < 0 else rc, "native checkpoint writer failed")
 
     def close(self) -> None:
         if self.h:

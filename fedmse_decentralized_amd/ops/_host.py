@@ -34,13 +34,17 @@ def lib():
                                                 ctypes.c_int32] + [ctypes.c_void_p] * 7 + [ctypes.c_int32,
                                                                                           ctypes.c_void_p,
                                                                                           ctypes.c_int32]
-            L.fedmx_writer_create.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
+            L.fedmx_writer_create.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                              ctypes.c_void_p, ctypes.c_int64]
             L.fedmx_writer_create.restype = ctypes.c_void_p
-            L.fedmx_writer_submit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32] + \
-                [ctypes.c_void_p] * 6 + [ctypes.c_int32]
+            L.fedmx_writer_submit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
             L.fedmx_writer_submit.restype = ctypes.c_int64
             L.fedmx_writer_wait.argtypes = [ctypes.c_void_p, ctypes.c_int64]
             L.fedmx_writer_wait.restype = ctypes.c_int32
+            L.fedmx_writer_flush.argtypes = [ctypes.c_void_p]
+            L.fedmx_writer_flush.restype = ctypes.c_int32
             L.fedmx_writer_destroy.argtypes = [ctypes.c_void_p]
             L.fedmx_writer_destroy.restype = None
             L.fedmx_map_file.argtypes = [ctypes.c_int32, ctypes.c_int64]

@@ -34,7 +34,10 @@
 #include <cstdint>
 #include <cstring>
 #include <deque>
+#include <fcntl.h>
 #include <mutex>
+#include <string>
+#include <unordered_map>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <thread>
@@ -224,23 +227,68 @@ namespace {
 struct WJob {
   const float* snap;
   int64_t stride;
-  std::vector<int32_t> rows, improved, fd_trk, trk_len;
-  std::vector<int64_t> cpt_dst;
+  std::vector<int32_t> rows, improved, trk_len;
+  std::vector<std::string> cpt_path, trk_path;
   std::vector<double> trk;
   int32_t trk_stride;
   int64_t ticket;
 };
 
+// mkdir -p of the directory holding `path` (a client's save directory)
+bool make_parents(const std::string& path) {
+  const size_t slash = path.rfind('/');
+  if (slash == std::string::npos || slash == 0) return false;
+  std::string dir = path.substr(0, slash);
+  for (size_t i = 1; i <= dir.size(); ++i) {
+    if (i == dir.size() || dir[i] == '/') {
+      const std::string part = dir.substr(0, i);
+      if (mkdir(part.c_str(), 0755) != 0 && errno != EEXIST) return false;
+    }
+  }
+  return true;
+}
+
+struct FileEnt {
+  int fd = -1;
+  uint8_t* map = nullptr;   // model.cpt: shared mapping of the whole file
+  int64_t size = -1;        // tracking: current file size (-1: unknown)
+};
+
 struct Writer {
   std::vector<int32_t> canon_idx;
   std::vector<int64_t> regions;
+  std::vector<uint8_t> tpl;   // legacy model.cpt template
   std::mutex mu;
   std::condition_variable cv_job, cv_done;
   std::deque<WJob> q;
   int64_t next_ticket = 0, done_ticket = 0;
   int32_t first_error = 0;
-  bool stop = false;
+  bool stop = false, release = false;
+  std::unordered_map<std::string, FileEnt> files;   // writer thread only
   std::thread th;
+
+  FileEnt* open_file(const std::string& path, int32_t& err) {
+    FileEnt& e = files[path];
+    if (e.fd < 0) {
+      e.fd = ::open(path.c_str(), O_RDWR | O_CREAT, 0644);
+      if (e.fd < 0 && errno == ENOENT && make_parents(path))
+        e.fd = ::open(path.c_str(), O_RDWR | O_CREAT, 0644);
+      if (e.fd < 0) {
+        if (!err) err = -errno;
+        files.erase(path);
+        return nullptr;
+      }
+    }
+    return &e;
+  }
+
+  void close_all() {
+    for (auto& kv : files) {
+      if (kv.second.map) munmap(kv.second.map, tpl.size());
+      if (kv.second.fd >= 0) ::close(kv.second.fd);
+    }
+    files.clear();
+  }
 
   void run() {
     std::vector<float> canon(canon_idx.size());
@@ -249,8 +297,18 @@ struct Writer {
       WJob job;
       {
         std::unique_lock<std::mutex> lk(mu);
-        cv_job.wait(lk, [&] { return stop || !q.empty(); });
-        if (q.empty()) return;
+        cv_job.wait(lk, [&] { return stop || release || !q.empty(); });
+        if (q.empty()) {
+          if (release) {
+            // every queued job is written: drop descriptors / mappings
+            close_all();
+            release = false;
+            cv_done.notify_all();
+            continue;
+          }
+          close_all();
+          return;
+        }
         job = std::move(q.front());
         q.pop_front();
       }
@@ -259,20 +317,37 @@ struct Writer {
       const int nreg = static_cast<int>(regions.size() / 3);
       for (int j = 0; j < n; ++j) {
         if (job.improved[j]) {
-          uint8_t* dst = reinterpret_cast<uint8_t*>(job.cpt_dst[j]);
-          const float* row = job.snap + static_cast<int64_t>(job.rows[j]) * job.stride;
-          for (size_t i = 0; i < canon.size(); ++i) canon[i] = row[canon_idx[i]];
-          for (int r = 0; r < nreg; ++r)
-            std::memcpy(dst + regions[3 * r], canon.data() + regions[3 * r + 2],
-                        static_cast<size_t>(regions[3 * r + 1]) * 4);
+          FileEnt* e = open_file(job.cpt_path[j], err);
+          if (e && !e->map) {
+            // first use: the file becomes the template, kept mapped
+            if (ftruncate(e->fd, static_cast<off_t>(tpl.size())) == 0) {
+              void* m = mmap(nullptr, tpl.size(), PROT_READ | PROT_WRITE, MAP_SHARED, e->fd, 0);
+              if (m != MAP_FAILED) {
+                e->map = static_cast<uint8_t*>(m);
+                std::memcpy(e->map, tpl.data(), tpl.size());
+              }
+            }
+            if (!e->map && !err) err = -EIO;
+          }
+          if (e && e->map) {
+            const float* row = job.snap + static_cast<int64_t>(job.rows[j]) * job.stride;
+            for (size_t i = 0; i < canon.size(); ++i) canon[i] = row[canon_idx[i]];
+            for (int r = 0; r < nreg; ++r)
+              std::memcpy(e->map + regions[3 * r], canon.data() + regions[3 * r + 2],
+                          static_cast<size_t>(regions[3 * r + 1]) * 4);
+          }
         }
         if (!pickle_tracking(job.trk.data() + static_cast<int64_t>(j) * job.trk_stride * 2, job.trk_len[j], pk)) {
           if (!err) err = -1;
           continue;
         }
-        struct stat st;
-        int64_t old = fstat(job.fd_trk[j], &st) == 0 ? static_cast<int64_t>(st.st_size) : 0;
-        const int rc = write_all(job.fd_trk[j], pk.data(), pk.size(), &old);
+        FileEnt* e = open_file(job.trk_path[j], err);
+        if (!e) continue;
+        if (e->size < 0) {
+          struct stat st;
+          e->size = fstat(e->fd, &st) == 0 ? static_cast<int64_t>(st.st_size) : 0;
+        }
+        const int rc = write_all(e->fd, pk.data(), pk.size(), &e->size);
         if (rc && !err) err = rc;
       }
       {
@@ -287,17 +362,22 @@ struct Writer {
 
 }  // namespace
 
-void* fedmx_writer_create(const int32_t* canon_idx, int32_t n_canon, const int64_t* regions, int32_t n_regions) {
+void* fedmx_writer_create(const int32_t* canon_idx, int32_t n_canon, const int64_t* regions, int32_t n_regions,
+                          const uint8_t* tpl, int64_t tpl_len) {
   Writer* w = new Writer();
   w->canon_idx.assign(canon_idx, canon_idx + n_canon);
   w->regions.assign(regions, regions + 3 * static_cast<int64_t>(n_regions));
+  w->tpl.assign(tpl, tpl + tpl_len);
   w->th = std::thread([w] { w->run(); });
   return w;
 }
 
-// Queue one round's checkpoint job; returns its ticket (> 0).
+// Queue one round's checkpoint job; returns its ticket (> 0).  Paths are
+// NUL-separated in `paths` (2n entries: model.cpt, tracking, per client);
+// the writer thread opens / creates / maps the files itself, so the caller
+// never waits on the filesystem.
 int64_t fedmx_writer_submit(void* handle, const float* snap, int64_t stride, int32_t n, const int32_t* rows,
-                            const int32_t* improved, const int64_t* cpt_dst, const int32_t* fd_trk, const double* trk,
+                            const int32_t* improved, const char* paths, int64_t paths_len, const double* trk,
                             const int32_t* trk_len, int32_t trk_stride) {
   Writer* w = static_cast<Writer*>(handle);
   WJob job;
@@ -305,18 +385,27 @@ int64_t fedmx_writer_submit(void* handle, const float* snap, int64_t stride, int
   job.stride = stride;
   job.rows.assign(rows, rows + n);
   job.improved.assign(improved, improved + n);
-  job.cpt_dst.assign(cpt_dst, cpt_dst + n);
-  job.fd_trk.assign(fd_trk, fd_trk + n);
   job.trk_len.assign(trk_len, trk_len + n);
   job.trk.assign(trk, trk + static_cast<int64_t>(n) * trk_stride * 2);
   job.trk_stride = trk_stride;
+  job.cpt_path.reserve(n);
+  job.trk_path.reserve(n);
+  const char* p = paths;
+  const char* end = paths + paths_len;
+  for (int j = 0; j < 2 * n && p < end; ++j) {
+    const size_t len = strnlen(p, static_cast<size_t>(end - p));
+    (j % 2 == 0 ? job.cpt_path : job.trk_path).emplace_back(p, len);
+    p += len + 1;
+  }
+  if (static_cast<int>(job.trk_path.size()) != n) return -1;
+  int64_t t;
   {
     std::lock_guard<std::mutex> lk(w->mu);
-    job.ticket = ++w->next_ticket;
+    t = job.ticket = ++w->next_ticket;
     w->q.push_back(std::move(job));
   }
   w->cv_job.notify_one();
-  return w->next_ticket;
+  return t;
 }
 
 // Block until job `ticket` (and every earlier one) is written; ticket <= 0:
@@ -326,6 +415,19 @@ int32_t fedmx_writer_wait(void* handle, int64_t ticket) {
   std::unique_lock<std::mutex> lk(w->mu);
   const int64_t t = ticket > 0 ? ticket : w->next_ticket;
   w->cv_done.wait(lk, [&] { return w->done_ticket >= t; });
+  return w->first_error;
+}
+
+// Every queued job written, then the writer thread closes its descriptors and
+// mappings (end of a sweep combination).  Returns the first write error.
+int32_t fedmx_writer_flush(void* handle) {
+  Writer* w = static_cast<Writer*>(handle);
+  std::unique_lock<std::mutex> lk(w->mu);
+  const int64_t t = w->next_ticket;
+  w->cv_done.wait(lk, [&] { return w->done_ticket >= t; });
+  w->release = true;
+  w->cv_job.notify_one();
+  w->cv_done.wait(lk, [&] { return !w->release; });
   return w->first_error;
 }
 

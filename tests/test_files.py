@@ -122,6 +122,10 @@ def test_native_async_writer_matches_python_writers(tmp_path):
                 ckpt.save_model_cpt_fast(ref[j], slots[si][rows[j]][cidx], DEFAULT_DIMS)
             ckpt.save_tracking(ref[j], trks[j])
         tickets[si] = w.submit(nat, slots[si], rows, improved, trks)
+        if rnd == 3:
+            # the writer thread releases its descriptors / mappings and
+            # reopens the existing files on the next job
+            w.flush()
     w.flush()
     for a, b in zip(nat, ref):
         for name in ("model.cpt", "training_tracking.pkl"):
