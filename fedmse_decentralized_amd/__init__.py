@@ -8,3 +8,9 @@ verification, early stop), ``parallel`` (RCCL/gloo/loopback comm, sharding),
 ``data``, ``eval``, ``io``, ``utils``.
 """
 __version__ = "0.1.0"
+
+# grow the descriptor table while the process is (usually) still
+# single-threaded: see io.files.reserve_fd_table
+from .io.files import reserve_fd_table as _reserve_fd_table  # noqa: E402
+
+_reserve_fd_table()

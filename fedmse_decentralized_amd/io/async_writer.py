@@ -112,6 +112,8 @@ class AsyncWriter:
             from .checkpoint import WRITE_STATS
             if WRITE_STATS:
                 print(f"  write_round_artifacts: {WRITE_STATS}", file=sys.stderr)
+            if self.native is not None:
+                print(f"  native writer thread: {self.native.stats()}", file=sys.stderr)
 
     def close(self):
         if self.enabled and self.t is not None:

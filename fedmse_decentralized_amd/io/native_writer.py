@@ -24,7 +24,7 @@ import numpy as np
 
 from ..models.layout import DEFAULT_DIMS, ModelDims, padded_index
 from . import checkpoint as ckpt
-from .files import ArtifactFiles
+from .files import ArtifactFiles, reserve_fd_table
 
 _MAX_NATIVE_EPOCHS = 1000   # the native pickler's single-batch limit
 
@@ -34,6 +34,7 @@ class NativeCheckpointWriter:
         from ..ops import _host
 
         self._lib = _host.lib()
+        reserve_fd_table()   # the writer thread keeps every client's files open
         self.dims = dims
         self.tpl = ckpt._template(dims)
         self.cidx = np.ascontiguousarray(padded_index(dims)[0].numpy(), dtype=np.int32)
@@ -84,6 +85,14 @@ class NativeCheckpointWriter:
             pc, pt = ckpt._artifact_paths(save_dir)
             b = self._paths[save_dir] = os.fsencode(pc) + b"\0" + os.fsencode(pt) + b"\0"
         return b
+
+    def stats(self) -> dict:
+        """The writer thread's own clock (ms) per phase, jobs and files opened."""
+        out = np.zeros(6, dtype=np.float64)
+        if self.h:
+            self._lib.fedmx_writer_stats(self.h, out.ctypes.data)
+        return {"open_ms": round(out[0], 3), "first_map_ms": round(out[1], 3), "patch_ms": round(out[2], 3),
+                "tracking_ms": round(out[3], 3), "jobs": int(out[4]), "files_opened": int(out[5])}
 
     def wait(self, ticket: int) -> None:
         rc = self._lib.fedmx_writer_wait(self.h, ticket)

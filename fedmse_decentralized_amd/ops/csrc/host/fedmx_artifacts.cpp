@@ -29,6 +29,8 @@
 // C ABI; loaded with ctypes from fedmse_decentralized_amd/ops/_host.py.
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cerrno>
 #include <condition_variable>
 #include <cstdint>
@@ -266,18 +268,44 @@ struct Writer {
   bool stop = false, release = false;
   std::unordered_map<std::string, FileEnt> files;   // writer thread only
   std::thread th;
+  // writer-thread clock, ns: [open/create, first map of model.cpt, parameter
+  // patch, tracking pickle + write, jobs, files opened]
+  std::atomic<int64_t> stat[6] = {};
+
+  static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
 
   FileEnt* open_file(const std::string& path, int32_t& err) {
     FileEnt& e = files[path];
     if (e.fd < 0) {
+      const int64_t t0 = now_ns();
       e.fd = ::open(path.c_str(), O_RDWR | O_CREAT, 0644);
       if (e.fd < 0 && errno == ENOENT && make_parents(path))
         e.fd = ::open(path.c_str(), O_RDWR | O_CREAT, 0644);
+      if (e.fd < 0 && errno == EMFILE) {
+        // descriptor limit: release every cached file, then retry
+        files.erase(path);
+        close_all();
+        FileEnt& f = files[path];
+        f.fd = ::open(path.c_str(), O_RDWR | O_CREAT, 0644);
+        if (f.fd < 0) {
+          if (!err) err = -errno;
+          files.erase(path);
+          return nullptr;
+        }
+        stat[0] += now_ns() - t0;
+        stat[5] += 1;
+        return &f;
+      }
       if (e.fd < 0) {
         if (!err) err = -errno;
         files.erase(path);
         return nullptr;
       }
+      stat[0] += now_ns() - t0;
+      stat[5] += 1;
     }
     return &e;
   }
@@ -319,6 +347,7 @@ struct Writer {
         if (job.improved[j]) {
           FileEnt* e = open_file(job.cpt_path[j], err);
           if (e && !e->map) {
+            const int64_t t0 = now_ns();
             // first use: the file becomes the template, kept mapped
             if (ftruncate(e->fd, static_cast<off_t>(tpl.size())) == 0) {
               void* m = mmap(nullptr, tpl.size(), PROT_READ | PROT_WRITE, MAP_SHARED, e->fd, 0);
@@ -328,15 +357,19 @@ struct Writer {
               }
             }
             if (!e->map && !err) err = -EIO;
+            stat[1] += now_ns() - t0;
           }
           if (e && e->map) {
+            const int64_t t0 = now_ns();
             const float* row = job.snap + static_cast<int64_t>(job.rows[j]) * job.stride;
             for (size_t i = 0; i < canon.size(); ++i) canon[i] = row[canon_idx[i]];
             for (int r = 0; r < nreg; ++r)
               std::memcpy(e->map + regions[3 * r], canon.data() + regions[3 * r + 2],
                           static_cast<size_t>(regions[3 * r + 1]) * 4);
+            stat[2] += now_ns() - t0;
           }
         }
+        const int64_t t1 = now_ns();
         if (!pickle_tracking(job.trk.data() + static_cast<int64_t>(j) * job.trk_stride * 2, job.trk_len[j], pk)) {
           if (!err) err = -1;
           continue;
@@ -349,7 +382,9 @@ struct Writer {
         }
         const int rc = write_all(e->fd, pk.data(), pk.size(), &e->size);
         if (rc && !err) err = rc;
+        stat[3] += now_ns() - t1;
       }
+      stat[4] += 1;
       {
         std::lock_guard<std::mutex> lk(mu);
         if (err && !first_error) first_error = err;
@@ -429,6 +464,16 @@ int32_t fedmx_writer_flush(void* handle) {
   w->cv_job.notify_one();
   w->cv_done.wait(lk, [&] { return !w->release; });
   return w->first_error;
+}
+
+// Writer-thread clock: out[0..5] = ms opening / creating files, ms first
+// mapping model.cpt files, ms patching parameters, ms pickling + writing
+// tracking (includes its opens), jobs done, files opened.
+void fedmx_writer_stats(void* handle, double* out) {
+  Writer* w = static_cast<Writer*>(handle);
+  for (int i = 0; i < 4; ++i) out[i] = 1e-6 * static_cast<double>(w->stat[i].load());
+  out[4] = static_cast<double>(w->stat[4].load());
+  out[5] = static_cast<double>(w->stat[5].load());
 }
 
 void fedmx_writer_destroy(void* handle) {

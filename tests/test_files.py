@@ -131,3 +131,19 @@ def test_native_async_writer_matches_python_writers(tmp_path):
         for name in ("model.cpt", "training_tracking.pkl"):
             assert open(os.path.join(a, name), "rb").read() == open(os.path.join(b, name), "rb").read()
     w.close()
+
+
+def test_fd_table_reserved_at_import():
+    """Importing the package grows the descriptor table (io.files.reserve_fd_table):
+    a descriptor near the top of the reserved range is usable at once."""
+    import fedmse_decentralized_amd  # noqa: F401
+    from fedmse_decentralized_amd.io import files
+
+    top = files.reserve_fd_table()
+    assert top >= 256
+    fd = os.open(os.devnull, os.O_RDONLY)
+    try:
+        os.dup2(fd, top - 1)
+        os.close(top - 1)
+    finally:
+        os.close(fd)
