@@ -43,6 +43,22 @@ METRIC = "rounds/sec + detection AUC, 10-client SAE (N-BaIoT shape) at 1/2/4/8 M
 EPISODE = 20   # paper schedule: 20 rounds per run; aggregation caps reset per episode
 
 
+def _collectives_label(comm) -> str:
+    """What carries the per-round exchange: RCCL (torch.distributed "nccl"
+    on ROCm), gloo, or nothing (one rank: in-process loopback)."""
+    if type(comm).__name__ == "PhantomComm":
+        return "collectives stubbed: one-GPU projection of rank 0"
+    try:
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized():
+            b = dist.get_backend()
+            return ("RCCL" if b == "nccl" else str(b)) + " all-gather/all-reduce"
+    except Exception:
+        pass
+    return "in-process loopback; RCCL all-gather/all-reduce at N > 1"
+
+
 def main(argv=None):
     # stdout carries exactly ONE line, the JSON record: native libraries'
     # chatter (RCCL prints a version banner to stdout when a communicator is
@@ -201,7 +217,7 @@ def _main(argv, real_stdout: int):
                          + (f"{args.clients} clients" if args.clients else f"{args.clients_per_gpu} clients/GPU"),
                 "global_batch": args.batch_size,
                 "seq_len": 115,
-                "parallelism": f"client-sharded x{n_gpus} (RCCL all-gather/all-reduce)",
+                "parallelism": f"client-sharded x{n_gpus} ({_collectives_label(comm)})",
                 "clients": fed.N,
                 "participation": 0.5,
                 "local_epochs": args.epochs,

@@ -94,3 +94,26 @@ def test_partition_devices_pipeline(tmp_path):
             tot[split] += arr.shape[0]
     # 5 % of 3 x 4000 benign = 600 (40 % held out), 5 % of 3 x 4000 attack = 600
     assert tot == {"normal": 360, "abnormal": 600, "test_normal": 240}
+
+
+def test_bench_two_ranks_under_torch_distributed_run():
+    """The driver's N > 1 launch (`python -m torch.distributed.run ...
+    bench.py --gpus 2`) on CPU with gloo: rank 0 alone prints one JSON line,
+    n_gpus = 2, a 20-client federation, the collectives named by backend."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+                        "--gpus", "2", "--backend", "torch", "--steps", "1", "--warmup", "0", "--epochs", "1",
+                        "--no-artifacts"], cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["clients"] == 20 and rec["value"] > 0
+    assert rec["config"]["parallelism"] == "client-sharded x2 (gloo all-gather/all-reduce)"
