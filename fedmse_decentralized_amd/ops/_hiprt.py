@@ -7,8 +7,14 @@ of microseconds each), the framework keeps two rings of *mapped, coherent*
 pinned host memory:
 
 * ``DescRing`` – the host writes descriptor arrays with a plain numpy copy and
-  passes the ring's *device* address to the kernel, which reads them over
-  PCIe at block start (zero copy, no API call);
+  passes the ring's *device* address to the kernel (zero copy, no API call).
+  The ring lives in fine-grained *device* memory that the host writes through
+  the PCIe BAR (write-combined stores, ~0.4 us per KB, then a store fence):
+  a kernel on the round's critical path then reads its descriptors from HBM
+  instead of paying ~1.2 us per dependent read of mapped host memory
+  (``scripts/probes/mapped_latency.hip``; host rewrites between launches are
+  always seen, ``scripts/probes/finegrained_host_write.hip``).
+  ``FEDMX_DESC_RING=host`` keeps it in mapped pinned host memory;
 * ``OutRing``  – kernels write host-visible results (scores, drifts, AUCs,
   training tracking) straight into it; the host reads them after the single
   ``hipStreamSynchronize`` that ends each protocol phase.
@@ -27,6 +33,7 @@ import numpy as np
 
 hipHostMallocMapped = 0x2
 hipHostMallocCoherent = 0x40000000
+hipDeviceMallocFinegrained = 0x1
 
 _lib = None
 _lock = threading.Lock()
@@ -57,6 +64,10 @@ def rt():
                 L.hipHostFree.restype = ctypes.c_int
                 L.hipDeviceSynchronize.argtypes = []
                 L.hipDeviceSynchronize.restype = ctypes.c_int
+                L.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_uint]
+                L.hipExtMallocWithFlags.restype = ctypes.c_int
+                L.hipFree.argtypes = [vp]
+                L.hipFree.restype = ctypes.c_int
                 _lib = L
     return _lib
 
@@ -116,9 +127,43 @@ class MappedBuffer:
             pass
 
 
+class DeviceWriteBuffer:
+    """Fine-grained device memory the host writes directly (large BAR): the
+    same address on both sides.  Host reads of it are slow (uncached PCIe
+    reads) — write-only from the host."""
+
+    def __init__(self, nbytes: int):
+        L = rt()
+        p = ctypes.c_void_p()
+        rc = L.hipExtMallocWithFlags(ctypes.byref(p), nbytes, hipDeviceMallocFinegrained)
+        if rc != 0 or not p.value:
+            raise RuntimeError(f"hipExtMallocWithFlags({nbytes}, fine-grained) failed ({rc})")
+        self.host_ptr = p.value
+        self.dev_ptr = p.value
+        self.nbytes = nbytes
+        self.np = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.host_ptr))
+
+    def __del__(self):
+        try:
+            if self.host_ptr and _lib is not None:
+                _lib.hipDeviceSynchronize()
+                _lib.hipFree(ctypes.c_void_p(self.host_ptr))
+            self.host_ptr = None
+        except Exception:
+            pass
+
+
+def _store_fence():
+    from . import _host
+
+    return _host.lib().fedmx_store_fence
+
+
 class _Ring:
+    buffer_type = MappedBuffer
+
     def __init__(self, nbytes: int, stream: int):
-        self.buf = MappedBuffer(nbytes)
+        self.buf = self.buffer_type(nbytes)
         self._retired = []   # replaced buffers stay alive (host views may still point into them)
         self.stream = stream
         self.off = 0
@@ -131,7 +176,7 @@ class _Ring:
             # the old ring, then replace it with one twice the request
             device_sync()
             self._retired.append(self.buf)
-            self.buf = MappedBuffer(2 * nbytes)
+            self.buf = self.buffer_type(2 * nbytes)
             self.off = 0
             self.wrap_gen = SyncClock.gen
         if self.off + nbytes > self.buf.nbytes:
@@ -147,6 +192,19 @@ class _Ring:
 
 
 class DescRing(_Ring):
+    def __init__(self, nbytes: int, stream: int, device_memory: Optional[bool] = None):
+        import os
+
+        if device_memory is None:
+            device_memory = os.environ.get("FEDMX_DESC_RING", "device") != "host"
+        self.fence = None
+        if device_memory:
+            self.buffer_type = DeviceWriteBuffer
+            # the host's write-combined stores must be visible before the
+            # launch that reads them is submitted
+            self.fence = _store_fence()
+        super().__init__(nbytes, stream)
+
     def put(self, *arrays: np.ndarray) -> List[int]:
         blobs = [np.ascontiguousarray(a).view(np.uint8).reshape(-1) for a in arrays]
         sizes = [(b.nbytes + 63) & ~63 for b in blobs]
@@ -156,6 +214,8 @@ class DescRing(_Ring):
             self.buf.np[o:o + b.nbytes] = b
             ptrs.append(self.buf.dev_ptr + o)
             o += s
+        if self.fence is not None:
+            self.fence()
         return ptrs
 
 

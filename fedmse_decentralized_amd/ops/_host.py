@@ -43,6 +43,8 @@ def lib():
             L.fedmx_writer_submit.restype = ctypes.c_int64
             L.fedmx_writer_wait.argtypes = [ctypes.c_void_p, ctypes.c_int64]
             L.fedmx_writer_wait.restype = ctypes.c_int32
+            L.fedmx_store_fence.argtypes = []
+            L.fedmx_store_fence.restype = None
             L.fedmx_writer_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
             L.fedmx_writer_stats.restype = None
             L.fedmx_writer_flush.argtypes = [ctypes.c_void_p]

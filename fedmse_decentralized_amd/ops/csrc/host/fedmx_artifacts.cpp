@@ -37,6 +37,7 @@
 #include <cstring>
 #include <deque>
 #include <fcntl.h>
+#include <immintrin.h>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -464,6 +465,14 @@ int32_t fedmx_writer_flush(void* handle) {
   w->cv_job.notify_one();
   w->cv_done.wait(lk, [&] { return !w->release; });
   return w->first_error;
+}
+
+// Full store fence: the host's write-combined stores into fine-grained
+// device memory (the descriptor ring, ops/_hiprt.py) are globally visible
+// before the kernel launch that reads them is submitted.
+void fedmx_store_fence() {
+  _mm_sfence();   // drains the write-combining buffers
+  std::atomic_thread_fence(std::memory_order_seq_cst);
 }
 
 // Writer-thread clock: out[0..5] = ms opening / creating files, ms first
