@@ -36,6 +36,7 @@ per round in both paths.
 from __future__ import annotations
 
 import logging
+import os
 import weakref
 from collections import deque
 from typing import Dict, List, Optional
@@ -125,11 +126,24 @@ class DeviceRound:
         self.side_slots = [dict(rep=torch.zeros(2 * N, dtype=f64, device=dev),
                                 params=torch.empty_like(st.params), best=torch.empty_like(st.best), ev=None)
                            for _ in range(NSIDE)]
-        # standardised vote data, by round parity.  Reuse needs no event of
-        # its own: round r+2's standardisation is queued on the side stream
-        # behind that stream's wait for round r+1's decisions, which the main
-        # stream records after round r's vote forward has read the buffer.
+        # standardised vote data (src/Trainer/client_trainer.py:220-223: the
+        # voter's validation set, re-standardised with its own ddof=1 column
+        # stats at every vote).  Each client's validation set is fixed for the
+        # whole run, so its standardised copy is computed once here for every
+        # client that can vote: the round then reads it with no standardisation
+        # launch and no cross-stream wait (that wait, a barrier packet on the
+        # main stream even when the side stream is long done, cost ~6 us per
+        # round between training and the vote forward).  Federations whose
+        # copies would not fit FEDMX_VOTE_CACHE_MB fall back to standardising
+        # per round on the side stream (by round parity: round r+2's
+        # standardisation is queued behind the side stream's wait for round
+        # r+1's decisions, recorded after round r's vote forward read it).
         self.vs_bufs = [None, None]
+        self.vs_cache = None
+        cache_mb = float(os.environ.get("FEDMX_VOTE_CACHE_MB", "2048"))
+        rows = sum(int(v.shape[0]) for v in fed.valid_all)
+        if fed.local and rows * int(fed.valid_all[0].shape[1]) * 4 <= cache_mb * (1 << 20):
+            self.vs_cache = [_hip.standardize_ddof1(v.contiguous(), fed.dims.d_in) for v in fed.valid_all]
         # best-model snapshots for the artefact writer: a ring of mapped host
         # slots filled by a device copy kernel (no torch pinned allocation or
         # blocking copy on the enqueue path); a slot is reused once the writer
@@ -178,6 +192,15 @@ class DeviceRound:
             self._vdata = vdata
             self.vx = torch.tensor([d.data_ptr() for d in vdata], dtype=torch.int64, device=dev)
         self.fused_verify = bool(fed.local) and max(int(d.shape[0]) for d in vdata) <= _hip.VERIFY_MAX_ROWS
+        # split verification (FEDMX_VERIFY_SPLIT=0: one workgroup per receiver):
+        # ~one 16-row tile per wave of 4-wave forward workgroups + a drift workgroup
+        self.verify_parts = 0
+        if self.fused_verify and os.environ.get("FEDMX_VERIFY_SPLIT", "1") != "0":
+            tiles = max((int(d.shape[0]) + 15) // 16 for d in vdata)
+            self.verify_parts = max(1, min(16, (tiles + 3) // 4))
+            self.v_sse = torch.zeros(self.n_local, _hip.VERIFY_MAX_ROWS, dtype=f32, device=dev)
+            self.v_drift = torch.zeros(self.n_local, dtype=f32, device=dev)
+            self.v_cnt = torch.zeros(self.n_local, dtype=i32, device=dev)
         self.rule = 1 if fed.update_type == "mse_avg" else 0
         self.pending: deque = deque()
         self.all_rounds: Dict[int, dict] = {}
@@ -203,7 +226,9 @@ class DeviceRound:
         rec = dict(round=rnd, selected=list(selected), local_sel=local_sel, done=False)
 
         ev_std = None
-        if local_sel:
+        if local_sel and self.vs_cache is not None:
+            vs = self.vs_cache[selected[0]]
+        elif local_sel:
             # the vote data does not depend on training: standardise it on the
             # side stream (double-buffered by round parity) while training runs
             vdata = fed.valid_all[selected[0]]
@@ -221,7 +246,8 @@ class DeviceRound:
             rec["handle"] = handle
         with tel.phase("vote"):
             if local_sel:
-                torch.cuda.current_stream(dev).wait_event(ev_std)
+                if ev_std is not None:
+                    torch.cuda.current_stream(dev).wait_event(ev_std)
                 need_dev = self.rule == 1
                 items = [(r, vs) for r in local_rows]
                 # each client's record [vote score, -, dev MSE, dev MSE] (4 doubles):
@@ -335,7 +361,13 @@ class DeviceRound:
                 v = _hip.VerifyArgs(D=d, vx=self.vx.data_ptr(), vn=self.vsse_n.data_ptr(),
                                     eval_params=eval_params.data_ptr(), best_stage=best_stage.data_ptr(),
                                     best=st.best.data_ptr(), latent=fed.dims.latent, hidden=fed.dims.hidden)
-                _hip.verify_decide(v, dev)
+                if self.verify_parts:
+                    _hip.verify_split(_hip.VerifySplitArgs(V=v, sse_g=self.v_sse.data_ptr(),
+                                                           drift_g=self.v_drift.data_ptr(),
+                                                           cnt=self.v_cnt.data_ptr(), parts=self.verify_parts,
+                                                           pad=0), dev)
+                else:
+                    _hip.verify_decide(v, dev)
             else:
                 _hip.decide_adopt(d, dev)
         slot_ptr, slot = self.rt.out.take(np.float64, 2 * N)
