@@ -192,15 +192,6 @@ class DeviceRound:
             self._vdata = vdata
             self.vx = torch.tensor([d.data_ptr() for d in vdata], dtype=torch.int64, device=dev)
         self.fused_verify = bool(fed.local) and max(int(d.shape[0]) for d in vdata) <= _hip.VERIFY_MAX_ROWS
-        # split verification (FEDMX_VERIFY_SPLIT=0: one workgroup per receiver):
-        # ~one 16-row tile per wave of 4-wave forward workgroups + a drift workgroup
-        self.verify_parts = 0
-        if self.fused_verify and os.environ.get("FEDMX_VERIFY_SPLIT", "1") != "0":
-            tiles = max((int(d.shape[0]) + 15) // 16 for d in vdata)
-            self.verify_parts = max(1, min(16, (tiles + 3) // 4))
-            self.v_sse = torch.zeros(self.n_local, _hip.VERIFY_MAX_ROWS, dtype=f32, device=dev)
-            self.v_drift = torch.zeros(self.n_local, dtype=f32, device=dev)
-            self.v_cnt = torch.zeros(self.n_local, dtype=i32, device=dev)
         self.rule = 1 if fed.update_type == "mse_avg" else 0
         self.pending: deque = deque()
         self.all_rounds: Dict[int, dict] = {}
@@ -361,13 +352,7 @@ class DeviceRound:
                 v = _hip.VerifyArgs(D=d, vx=self.vx.data_ptr(), vn=self.vsse_n.data_ptr(),
                                     eval_params=eval_params.data_ptr(), best_stage=best_stage.data_ptr(),
                                     best=st.best.data_ptr(), latent=fed.dims.latent, hidden=fed.dims.hidden)
-                if self.verify_parts:
-                    _hip.verify_split(_hip.VerifySplitArgs(V=v, sse_g=self.v_sse.data_ptr(),
-                                                           drift_g=self.v_drift.data_ptr(),
-                                                           cnt=self.v_cnt.data_ptr(), parts=self.verify_parts,
-                                                           pad=0), dev)
-                else:
-                    _hip.verify_decide(v, dev)
+                _hip.verify_decide(v, dev)
             else:
                 _hip.decide_adopt(d, dev)
         slot_ptr, slot = self.rt.out.take(np.float64, 2 * N)

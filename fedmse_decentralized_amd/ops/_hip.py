@@ -107,11 +107,6 @@ class VerifyArgs(ctypes.Structure):
                 ("best", _vp), ("latent", _i32), ("hidden", _i32)]
 
 
-class VerifySplitArgs(ctypes.Structure):
-    _fields_ = [("V", VerifyArgs), ("sse_g", _vp), ("drift_g", _vp), ("cnt", _vp), ("parts", _i32),
-                ("pad", _i32)]
-
-
 def lib():
     global _lib
     if _lib is not None:
@@ -139,7 +134,6 @@ def lib():
                 "fedmx_elect_wsum": [ctypes.POINTER(ElectArgs), ctypes.POINTER(WsumArgs), vp],
                 "fedmx_decide_adopt": [ctypes.POINTER(DecideArgs), vp],
                 "fedmx_verify_decide": [ctypes.POINTER(VerifyArgs), vp],
-                "fedmx_verify_split": [ctypes.POINTER(VerifySplitArgs), vp],
                 "fedmx_copy_f64": [vp, vp, i32, vp],
                 "fedmx_copy2_f64": [vp, vp, i32, vp, vp, i32, vp],
                 "fedmx_copy_rows": [vp, i32, vp, vp, i32, vp, i32, i32, vp],
@@ -154,10 +148,10 @@ def lib():
             assert L.fedmx_auc_desc_size() == AUC_DTYPE.itemsize
             assert L.fedmx_seg_desc_size() == SEG_DTYPE.itemsize
             assert L.fedmx_train_args_size() == ctypes.sizeof(TrainArgs)
-            sz = (ctypes.c_int * 5)()
+            sz = (ctypes.c_int * 4)()
             L.fedmx_protocol_sizes(ctypes.cast(sz, ctypes.c_void_p))
             assert tuple(sz) == (ctypes.sizeof(ElectArgs), ctypes.sizeof(WsumArgs), ctypes.sizeof(DecideArgs),
-                                 ctypes.sizeof(VerifyArgs), ctypes.sizeof(VerifySplitArgs)), tuple(sz)
+                                 ctypes.sizeof(VerifyArgs)), tuple(sz)
             _lib = L
     return _lib
 
@@ -505,12 +499,6 @@ def decide_adopt(args: DecideArgs, device):
 def verify_decide(args: VerifyArgs, device):
     """Verification forward + decide_adopt + evaluation snapshot, one launch."""
     _check(lib().fedmx_verify_decide(ctypes.byref(args), _stream(device)), "fedmx_verify_decide")
-
-
-def verify_split(args: VerifySplitArgs, device):
-    """verify_decide with each receiver spread over ``parts`` forward
-    workgroups + a drift workgroup; the last arriver decides (bit-identical)."""
-    _check(lib().fedmx_verify_split(ctypes.byref(args), _stream(device)), "fedmx_verify_split")
 
 
 def copy_f64(dst_ptr: int, src_ptr: int, n: int, device):

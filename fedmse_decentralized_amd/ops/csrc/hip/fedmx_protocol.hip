@@ -404,44 +404,44 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
       const double tot = s_d[0] + s_d[1] + s_d[2] + s_d[3];
       mse = n > 0 ? tot / ((double)n * A.d_in) : __builtin_nan("");
     }
-    // ---- drift of the receiver's history vs the aggregate (param_drift order)
+    // ---- drift of the receiver's history vs the aggregate (param_drift order:
+    // virtual threads vt = tid and tid + 512 of a 1024-thread block, each
+    // summing p = vt, vt + 1024, ... in increasing order).  All of a
+    // thread's loads are issued before the first add: one memory round trip
+    // instead of one per 4 elements (6 dependent rounds, ~5 us of the kernel).
     float drift = 0.f;
     if (had_hist) {
-      // virtual threads vt = tid and tid + 512 of a 1024-thread block
       const float* h = A.hist + off;
-      float acc[2][8];
+      constexpr int NJ = (P_PAD + 1023) / 1024;
+      int sg[2][NJ];
+      float df[2][NJ];
 #pragma unroll
       for (int q = 0; q < 2; ++q)
 #pragma unroll
-        for (int t = 0; t < 8; ++t) acc[q][t] = 0.f;
-      // four p's loads in flight per step, accumulated in increasing p
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-        for (int p0 = tid + 512 * q; p0 < A.P; p0 += 4096) {
-          int sg[4];
-          float df[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int p = p0 + 1024 * u;
-            sg[u] = -1;
-            df[u] = 0.f;
-            if (p < A.P) {
-              sg[u] = A.seg[p];
-              df[u] = h[p] - A.agg[p];
-            }
+        for (int j = 0; j < NJ; ++j) {
+          const int p = tid + 512 * q + 1024 * j;
+          sg[q][j] = -1;
+          df[q][j] = 0.f;
+          if (p < P_PAD) {
+            sg[q][j] = A.seg[p];
+            df[q][j] = h[p] - A.agg[p];
           }
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int t = 0; t < 8; ++t) acc[q][t] += (sg[u] == t) ? df[u] * df[u] : 0.0f;
         }
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int q = 0; q < 2; ++q) {
+        float acc[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = 0.f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int t = 0; t < 8; ++t) acc[t] += (sg[q][j] == t) ? df[q][j] * df[q][j] : 0.0f;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-          const float v = wave_sum(acc[q][t]);
+          const float v = wave_sum(acc[t]);
           if (lane == 0) part[t][wv + 8 * q] = v;
         }
+      }
       __syncthreads();
       if (tid == 0) {
         float tot = 0.f;
@@ -497,204 +497,6 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
       if (receiver) reinterpret_cast<f32x4*>(A.hist + off)[i] = v[u];
       evp[i] = pv[u];
       bst[i] = bv[u];
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Split verification: the fused verification above with each receiver's work
-// spread over `parts` forward workgroups (a contiguous range of its 16-row
-// tiles each, per-row SSE to global memory) plus one drift workgroup (drift
-// of the history vs the aggregate, then the decision-independent history and
-// best-model snapshot writes).  The last of a receiver's parts + 1 workgroups
-// to arrive (agent-scope release / ticket / acquire) reduces the MSE, takes
-// the decision and writes the decision-dependent rows.  Every reduction keeps
-// the arithmetic and order of verify_decide_kernel (the drift block plays the
-// 1024 threads of param_drift as 4 x 256; the MSE is the same 256-thread
-// strided sum), so results are bit-identical; the forward of a receiver's
-// ~180 rows no longer runs on 8 waves of ONE workgroup behind the drift.
-struct VerifySplitArgs {
-  VerifyArgs V;
-  float* sse_g;       // [n_local][VERIFY_MAX_ROWS] per-row SSE of the aggregate
-  float* drift_g;     // [n_local]
-  int32_t* cnt;       // [n_local] arrival tickets: zero between launches (the last arriver resets)
-  int32_t parts;      // forward workgroups per receiver; grid = n_local * (parts + 1)
-  int32_t pad;
-};
-static_assert(sizeof(VerifySplitArgs) == sizeof(VerifyArgs) + 32, "VerifySplitArgs layout is shared with Python");
-
-__global__ __launch_bounds__(256) void verify_split_kernel(const VerifySplitArgs S) {
-  const VerifyArgs& V = S.V;
-  const DecideArgs& A = V.D;
-  __shared__ __attribute__((aligned(16))) float sW1[HP * S_W1];
-  __shared__ __attribute__((aligned(16))) float sW2[ZP * S_W2];
-  __shared__ __attribute__((aligned(16))) float sW3[HP * S_W3];
-  __shared__ __attribute__((aligned(16))) float sW4[DP * S_W4];
-  __shared__ int s_flag;
-  __shared__ double s_d[4];
-  __shared__ float part[8][16];
-  const int a = A.state[0];
-  if (a >= 0 && blockIdx.x == 0 && threadIdx.x == 0) A.agg_counts[a] += 1;
-  const int nper = S.parts + 1;
-  const int cl = blockIdx.x / nper;
-  const int pt = blockIdx.x - cl * nper;
-  if (cl >= A.n_local) return;
-  const int c = A.start + cl;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wv = tid >> 6;
-  const size_t off = (size_t)cl * A.P;
-  const int n4 = A.P / 4;
-  const f32x4* src = reinterpret_cast<const f32x4*>(A.agg);
-  f32x4* prm = reinterpret_cast<f32x4*>(A.params + off);
-  f32x4* evp = reinterpret_cast<f32x4*>(V.eval_params + off);
-  f32x4* bst = reinterpret_cast<f32x4*>(V.best_stage + off);
-  const f32x4* bsrc = reinterpret_cast<const f32x4*>(V.best + off);
-  if (a < 0 || c == a) {
-    // no aggregator: snapshots only; the aggregator loads its aggregate
-    // (anchor / history unchanged).  One workgroup per client.
-    if (pt != 0) return;
-    for (int i = tid; i < n4; i += 256) {
-      const f32x4 v = (a >= 0) ? src[i] : prm[i];
-      if (a >= 0) prm[i] = v;
-      evp[i] = v;
-      bst[i] = bsrc[i];
-    }
-    return;
-  }
-  const int n = V.vn[cl];
-  float* sse = S.sse_g + (size_t)cl * VERIFY_MAX_ROWS;
-  if (pt < S.parts) {
-    // ---- a contiguous range of the receiver's 16-row tiles (fwd_rows arithmetic)
-    const int ntiles = (n + 15) >> 4;
-    const int tpp = (ntiles + S.parts - 1) / S.parts;
-    const int r0 = 16 * tpp * pt;
-    const int r1 = min(n, 16 * tpp * (pt + 1));
-    if (r0 < r1) {
-      stage_params(A.agg, sW1, sW2, sW3, sW4);
-      __syncthreads();
-      FwdDesc d;
-      d.params = A.agg;
-      d.x = reinterpret_cast<const float*>(V.vx[cl]) + (size_t)r0 * DP;
-      d.sse = sse + r0;
-      d.lat = nullptr;
-      d.nrows = r1 - r0;
-      d.lat_stride = V.latent;
-      d.d_in = A.d_in;
-      d.latent = V.latent;
-      d.hidden = V.hidden;
-      fwd_rows_block(d, sW1, sW2, sW3, sW4, wv, 4, d.sse);
-    }
-  } else {
-    // ---- drift of the receiver's history vs the aggregate (param_drift order:
-    // virtual threads vt = tid + 256 q of a 1024-thread block), then the
-    // decision-independent writes: history <- aggregate, best-model snapshot
-    if (A.has_hist[cl]) {
-      const float* h = A.hist + off;
-      float acc[4][8];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int t = 0; t < 8; ++t) acc[q][t] = 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        for (int p0 = tid + 256 * q; p0 < A.P; p0 += 4096) {
-          int sg[4];
-          float df[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int p = p0 + 1024 * u;
-            sg[u] = -1;
-            df[u] = 0.f;
-            if (p < A.P) {
-              sg[u] = A.seg[p];
-              df[u] = h[p] - A.agg[p];
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int t = 0; t < 8; ++t) acc[q][t] += (sg[u] == t) ? df[u] * df[u] : 0.0f;
-        }
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const float v = wave_sum(acc[q][t]);
-          if (lane == 0) part[t][wv + 4 * q] = v;
-        }
-      __syncthreads();
-      if (tid == 0) {
-        float tot = 0.f;
-        for (int t = 0; t < 8; ++t) {
-          float s2 = 0.f;
-          for (int w = 0; w < 16; ++w) s2 += part[t][w];
-          tot += sqrtf(s2);
-        }
-        S.drift_g[cl] = tot;
-      }
-      __syncthreads();   // every wave has read the old history
-    }
-    f32x4* hst = reinterpret_cast<f32x4*>(A.hist + off);
-    for (int i = tid; i < n4; i += 256) {
-      hst[i] = src[i];
-      bst[i] = bsrc[i];
-    }
-  }
-  // ---- publish (agent-scope release), draw a ticket; the last arriver goes on
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(&S.cnt[cl], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_flag = (t == S.parts);
-    if (t == S.parts) {
-      S.cnt[cl] = 0;   // ready for the next launch
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!s_flag) return;
-  const int had_hist = A.has_hist[cl];
-  // ---- MSE (score_reduce / decide_adopt order)
-  double mse;
-  {
-    double sv = 0.0;
-#pragma unroll 8
-    for (int r = tid; r < n; r += 256) sv += (double)sse[r];
-    for (int o = 32; o >= 1; o >>= 1) sv += __shfl_xor(sv, o, 64);
-    if (lane == 0) s_d[wv] = sv;
-    __syncthreads();
-    const double tot = s_d[0] + s_d[1] + s_d[2] + s_d[3];
-    mse = n > 0 ? tot / ((double)n * A.d_in) : __builtin_nan("");
-  }
-  if (tid == 0) {
-    const double perf = 1.0 / (1.0 + mse);
-    int okk;
-    if (!had_hist) {
-      okk = 1;  // the first received model is accepted unconditionally
-      A.has_hist[cl] = 1;
-    } else {
-      const double change = perf - A.hist_perf[cl];
-      okk = ((double)S.drift_g[cl] <= A.thr) && (change >= -A.pthr);
-    }
-    A.hist_perf[cl] = perf;
-    const int rj = okk ? 0 : A.rejected[cl] + 1;
-    A.rejected[cl] = rj;
-    A.rej_out[c] = (double)rj;
-    s_flag = okk;
-  }
-  __syncthreads();
-  const bool ok = s_flag != 0;
-  for (int i = tid; i < n4; i += 256) {
-    if (ok) {
-      const f32x4 v = src[i];
-      prm[i] = v;
-      reinterpret_cast<f32x4*>(A.anchor + off)[i] = v;
-      evp[i] = v;
-    } else {
-      evp[i] = prm[i];
     }
   }
 }
@@ -777,15 +579,6 @@ int fedmx_verify_decide(const void* args, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-int fedmx_verify_split(const void* args, hipStream_t stream) {
-  const fedmx::VerifySplitArgs& S = *reinterpret_cast<const fedmx::VerifySplitArgs*>(args);
-  const fedmx::DecideArgs& D = S.V.D;
-  if (D.P % 4 != 0 || D.P != fedmx::P_PAD || S.parts < 1 || S.parts > 64) return -1;
-  const int nl = D.n_local > 0 ? D.n_local : 1;
-  hipLaunchKernelGGL(fedmx::verify_split_kernel, dim3(nl * (S.parts + 1)), dim3(256), 0, stream, S);
-  return (int)hipGetLastError();
-}
-
 int fedmx_copy_f64(double* dst, const double* src, int n, hipStream_t stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(fedmx::copy_f64_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, dst, src, n);
@@ -797,7 +590,6 @@ int fedmx_protocol_sizes(int* out) {
   out[1] = (int)sizeof(fedmx::WsumArgs);
   out[2] = (int)sizeof(fedmx::DecideArgs);
   out[3] = (int)sizeof(fedmx::VerifyArgs);
-  out[4] = (int)sizeof(fedmx::VerifySplitArgs);
   return 0;
 }
 

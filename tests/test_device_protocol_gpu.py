@@ -206,25 +206,3 @@ def test_rccl_one_rank_forced_collectives_match_loopback(tmp_path):
     assert forced["config"]["device_protocol"] and base["config"]["device_protocol"]
     assert forced["detection_auc_mean"] == base["detection_auc_mean"]
     assert forced["detection_auc_min"] == base["detection_auc_min"]
-
-
-@pytest.mark.parametrize("update_type", ["mse_avg", "fedprox"])
-def test_split_verification_matches_one_workgroup_kernel(tmp_path, monkeypatch, update_type):
-    """verify_split_kernel (each receiver over several forward workgroups + a
-    drift workgroup, last-arriver decision) leaves bit-identical decisions,
-    parameters, FedProx anchors, histories and metrics to the one-workgroup
-    fused verification kernel (FEDMX_VERIFY_SPLIT=0).  1,500-1,700 normal
-    rows per client: ~150-170 verification rows -> 3 forward parts each."""
-    _shrink()
-    monkeypatch.setitem(SHRINK, "normal_rows", (1500, 1700))
-    monkeypatch.setenv("FEDMX_VERIFY_SPLIT", "0")
-    fa, a = _run(_cfg(str(tmp_path / "a"), save_checkpoints=False, epoch=1, network_size=10), update_type, 5)
-    assert fa._fast is not None and fa._fast.verify_parts == 0
-    monkeypatch.setenv("FEDMX_VERIFY_SPLIT", "1")
-    fb, b = _run(_cfg(str(tmp_path / "b"), save_checkpoints=False, epoch=1, network_size=10), update_type, 5)
-    assert fb._fast.verify_parts >= 2
-    assert a == b
-    for name in ("params", "adam_m", "adam_v", "anchor", "best"):
-        assert torch.equal(getattr(fa.engine.store, name), getattr(fb.engine.store, name)), name
-    for name in ("hist", "has_hist", "hist_perf", "rejected", "agg_counts"):
-        assert torch.equal(getattr(fa._fast, name), getattr(fb._fast, name)), name
