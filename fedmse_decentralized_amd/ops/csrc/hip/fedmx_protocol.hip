@@ -60,6 +60,7 @@ static_assert(sizeof(WsumArgs) == 48, "WsumArgs layout is shared with Python");
 // aggregate.  Workgroup 0 publishes the aggregator / voter / weights; the
 // aggregation-cap count is bumped later by decide_adopt (a single writer,
 // after every workgroup here has read the counts).
+template <bool WIDE>
 __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, const WsumArgs W) {
   __shared__ float s_w[1024];
   __shared__ int64_t s_rows[1024];
@@ -182,6 +183,28 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
   }
   __syncthreads();
   if (s_agg < 0) return;
+  if (WIDE) {
+    // large selections (k > 8, e.g. the 8-rank job's 40): one element per
+    // thread and up to 64 selected rows' loads in flight before the first
+    // add — the float4 form below waits for 5 dependent rounds at k = 40
+    // (20.1 -> 13.2 us); for k <= 8 the float4 form is faster (6.5 vs 8.5 us)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= W.P) return;
+    constexpr int U = 64;
+    float acc = 0.f;
+    for (int k0 = 0; k0 < W.k; k0 += U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (k0 + u < W.k) v[u] = W.base[(size_t)s_rows[k0 + u] * W.P + i];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (k0 + u < W.k)
+          acc = (k0 + u == 0) ? __fmul_rn(v[u], s_w[k0 + u]) : __fadd_rn(acc, __fmul_rn(v[u], s_w[k0 + u]));
+    }
+    W.out[i] = acc;
+    return;
+  }
   const int i = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= W.P) return;
   // eight independent row loads in flight, added strictly in selection order
@@ -567,8 +590,10 @@ int fedmx_elect_wsum(const void* eargs, const void* wargs, hipStream_t stream) {
   const fedmx::ElectArgs& E = *reinterpret_cast<const fedmx::ElectArgs*>(eargs);
   const fedmx::WsumArgs& W = *reinterpret_cast<const fedmx::WsumArgs*>(wargs);
   if (W.P % 4 != 0 || W.k < 1 || E.k > 1024) return -1;
-  const int n4 = W.P / 4;
-  hipLaunchKernelGGL(fedmx::elect_wsum_kernel, dim3((n4 + 255) / 256), dim3(256), 0, stream, E, W);
+  if (W.k > 8)
+    hipLaunchKernelGGL(fedmx::elect_wsum_kernel<true>, dim3((W.P + 255) / 256), dim3(256), 0, stream, E, W);
+  else
+    hipLaunchKernelGGL(fedmx::elect_wsum_kernel<false>, dim3((W.P / 4 + 255) / 256), dim3(256), 0, stream, E, W);
   return (int)hipGetLastError();
 }
 

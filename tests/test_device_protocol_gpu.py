@@ -206,3 +206,19 @@ def test_rccl_one_rank_forced_collectives_match_loopback(tmp_path):
     assert forced["config"]["device_protocol"] and base["config"]["device_protocol"]
     assert forced["detection_auc_mean"] == base["detection_auc_mean"]
     assert forced["detection_auc_min"] == base["detection_auc_min"]
+
+
+def test_device_round_matches_host_path_large_selection(tmp_path):
+    """24 clients (12 selections per round: the election kernel's
+    one-element-per-thread aggregation path, k > 8) against the host path's
+    weighted_sum_kernel: identical aggregators, decisions and parameters."""
+    _shrink()
+    fa, a = _run(_cfg(str(tmp_path / "dev"), device_protocol=True, network_size=24, save_checkpoints=False),
+                 "mse_avg", 4)
+    fb, b = _run(_cfg(str(tmp_path / "host"), device_protocol=False, network_size=24, save_checkpoints=False),
+                 "mse_avg", 4)
+    assert fa._fast is not None and fb._fast is None
+    assert len(a["sel"][0]) == 12
+    assert a["sel"] == b["sel"] and a["agg"] == b["agg"] and a["ver"] == b["ver"]
+    assert torch.equal(fa.engine.store.params, fb.engine.store.params)
+    assert torch.equal(fa.engine.store.anchor, fb.engine.store.anchor)
