@@ -23,9 +23,15 @@ __global__ __launch_bounds__(256) void fwd_rows_kernel(const FwdDesc* __restrict
 
   const FwdDesc d = descs[blockIdx.x];
   if (d.nrows <= 0) return;   // alignment filler of an XCD-grouped descriptor list (whole block)
-  stage_params(d.params, sW1, sW2, sW3, sW4);
-  __syncthreads();
-  fwd_rows_block(d, sW1, sW2, sW3, sW4, threadIdx.x >> 6, 4, d.sse);
+  if (fwd_compact_ok(d)) {
+    stage_params<true>(d.params, sW1, sW2, sW3, sW4);
+    __syncthreads();
+    fwd_rows_block<true>(d, sW1, sW2, sW3, sW4, threadIdx.x >> 6, 4, d.sse);
+  } else {
+    stage_params<false>(d.params, sW1, sW2, sW3, sW4);
+    __syncthreads();
+    fwd_rows_block<false>(d, sW1, sW2, sW3, sW4, threadIdx.x >> 6, 4, d.sse);
+  }
 }
 
 // ---------------------------------------------------------------------------

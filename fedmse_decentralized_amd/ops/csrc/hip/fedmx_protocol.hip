@@ -368,6 +368,7 @@ struct VerifyArgs {
 };
 static_assert(sizeof(VerifyArgs) == sizeof(DecideArgs) + 48, "VerifyArgs layout is shared with Python");
 
+template <bool CP>
 __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) {
   const DecideArgs& A = V.D;
   __shared__ __attribute__((aligned(16))) float sW1[HP * S_W1];
@@ -398,8 +399,6 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
   } else if (a >= 0) {
     const int had_hist = A.has_hist[cl];
     // ---- SSE rows of the aggregate on this receiver's data (fwd_rows arithmetic)
-    stage_params(A.agg, sW1, sW2, sW3, sW4);
-    __syncthreads();
     FwdDesc d;
     d.params = A.agg;
     d.x = reinterpret_cast<const float*>(V.vx[cl]);
@@ -410,7 +409,9 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     d.d_in = A.d_in;
     d.latent = V.latent;
     d.hidden = V.hidden;
-    fwd_rows_block(d, sW1, sW2, sW3, sW4, wv, 8, s_sse);
+    stage_params<CP>(A.agg, sW1, sW2, sW3, sW4);
+    __syncthreads();
+    fwd_rows_block<CP>(d, sW1, sW2, sW3, sW4, wv, 8, s_sse);
     __syncthreads();
     // ---- MSE (score_reduce / decide_adopt order)
     double mse;
@@ -600,7 +601,12 @@ int fedmx_elect_wsum(const void* eargs, const void* wargs, hipStream_t stream) {
 int fedmx_verify_decide(const void* args, hipStream_t stream) {
   const fedmx::VerifyArgs& V = *reinterpret_cast<const fedmx::VerifyArgs*>(args);
   if (V.D.P % 4 != 0 || V.D.P != fedmx::P_PAD) return -1;
-  hipLaunchKernelGGL(fedmx::verify_decide_kernel, dim3(V.D.n_local > 0 ? V.D.n_local : 1), dim3(512), 0, stream, V);
+  const dim3 grid(V.D.n_local > 0 ? V.D.n_local : 1);
+  // compact forward order for the reference shapes (fedmx_forward_common.h)
+  if (V.D.d_in <= 115 && V.hidden <= 27 && V.latent <= 7)
+    hipLaunchKernelGGL(fedmx::verify_decide_kernel<true>, grid, dim3(512), 0, stream, V);
+  else
+    hipLaunchKernelGGL(fedmx::verify_decide_kernel<false>, grid, dim3(512), 0, stream, V);
   return (int)hipGetLastError();
 }
 
