@@ -238,20 +238,31 @@ class on_stream:
 
 
 # ---------------------------------------------------------------------------
-FWD_BLOCK_SLOTS = 4 * 256   # resident fwd_rows workgroups on an MI355X (40 KB LDS each, 4 per CU, 256 CUs)
+FWD_BLOCK_SLOTS = 4 * 256   # fwd_rows workgroups the LDS admits at once (40 KB each, 4 per CU, 256 CUs)
+FWD_RESIDENT = 2 * 256      # ... and the VGPRs (~197 per lane: 2 waves per SIMD -> 2 workgroups per CU)
 
 
 def fwd_rows_per_block(total_rows: int, n_items: int) -> int:
-    """Rows per fwd_rows workgroup (multiple of 64): as many workgroups as
-    the chip holds at once, never a sliver of a second wave of them — a
-    5 x 52,800-row dev-set scoring at 256 rows per block is 1,035 blocks,
-    11 of which would run alone after the first 1,024."""
+    """Rows per fwd_rows workgroup (multiple of 64): about one workgroup per
+    LDS slot, then grown while the block count would leave only a sliver of
+    workgroups for a last wave of residency (the headline's 33.8 K vote /
+    dev rows: 535 blocks of 64 rows -> 265 of 128, the 23 blocks past the
+    first 512 ran alone; -0.25 % round time).  Big scorings keep small
+    blocks (8-rank dev set: 836 blocks of 320 rows beat 460 of 576)."""
     fixed = int(os.environ.get("FEDMX_FWD_ROWS_PER_BLOCK", "0"))   # A/B override
     if fixed > 0:
         return fixed
     slots = max(FWD_BLOCK_SLOTS - n_items, 1)
     per = -(-int(total_rows) // slots)
     per = max(64, -(-per // 64) * 64)
+
+    def blocks(rpb):
+        return -(-int(total_rows) // rpb) + n_items
+
+    waves = blocks(per) / FWD_RESIDENT
+    if waves > 1 and waves - int(waves) < 0.25:
+        while blocks(per) > FWD_RESIDENT * int(waves):
+            per += 64
     return int(per)
 
 

@@ -111,14 +111,14 @@ __device__ __forceinline__ void stage_param4(float* sW1, float* sW2, float* sW3,
 }
 
 // The parameter vector (2,304 float4) is staged with all of a thread's
-// loads issued before its LDS writes: 2-3 global round trips per workgroup
-// instead of one per 256 / 512 elements.
+// loads issued before its LDS writes: one global round trip per workgroup of
+// >= 256 threads (9 float4 per thread) instead of one per 256 / 512 elements.
 template <bool CP>
 __device__ __forceinline__ void stage_params(const float* __restrict__ p, float* sW1, float* sW2, float* sW3,
                                              float* sW4) {
   const f32x4* p4 = reinterpret_cast<const f32x4*>(p);
   constexpr int N4 = P_PAD / 4;
-  constexpr int U = 4;
+  constexpr int U = (N4 + 255) / 256;
   const int nt = blockDim.x;
   for (int i0 = threadIdx.x; i0 < N4; i0 += U * nt) {
     f32x4 v[U];
