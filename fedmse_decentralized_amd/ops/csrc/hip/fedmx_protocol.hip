@@ -368,6 +368,12 @@ struct VerifyArgs {
 };
 static_assert(sizeof(VerifyArgs) == sizeof(DecideArgs) + 48, "VerifyArgs layout is shared with Python");
 
+// FEDMX_VERIFY_ABLATE (timing-only builds, wrong results; scripts/r2_verify_ablate.sh
+// after `python scripts/ab_variants.py build vabl1 vabl2 vabl4`): 1 no forward,
+// 2 no drift, 4 no adoption / snapshot pass
+#ifndef FEDMX_VERIFY_ABLATE
+#define FEDMX_VERIFY_ABLATE 0
+#endif
 template <bool CP>
 __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) {
   const DecideArgs& A = V.D;
@@ -409,9 +415,11 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     d.d_in = A.d_in;
     d.latent = V.latent;
     d.hidden = V.hidden;
-    stage_params<CP>(A.agg, sW1, sW2, sW3, sW4);
-    __syncthreads();
-    fwd_rows_block<CP>(d, sW1, sW2, sW3, sW4, wv, 8, s_sse);
+    if (!(FEDMX_VERIFY_ABLATE & 1)) {
+      stage_params<CP>(A.agg, sW1, sW2, sW3, sW4);
+      __syncthreads();
+      fwd_rows_block<CP>(d, sW1, sW2, sW3, sW4, wv, 8, s_sse);
+    }
     __syncthreads();
     // ---- MSE (score_reduce / decide_adopt order)
     double mse;
@@ -434,7 +442,7 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     // thread's loads are issued before the first add: one memory round trip
     // instead of one per 4 elements (6 dependent rounds, ~5 us of the kernel).
     float drift = 0.f;
-    if (had_hist) {
+    if (had_hist && !(FEDMX_VERIFY_ABLATE & 2)) {
       const float* h = A.hist + off;
       constexpr int NJ = (P_PAD + 1023) / 1024;
       int sg[2][NJ];
@@ -498,6 +506,7 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     load = ok;
   }
   // ---- adoption + history + snapshots in one pass over the row
+  if (FEDMX_VERIFY_ABLATE & 4) return;
   const bool receiver = a >= 0 && c != a;
   constexpr int UA = (P_PAD / 4 + 511) / 512;   // every element of the row in one pass of loads
   f32x4 v[UA], pv[UA], bv[UA];

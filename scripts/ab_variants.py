@@ -47,6 +47,10 @@ VARIANTS = {
     "abl_w1adam": ["-DFEDMX_ABLATE=2"],           # no W1 Adam                0.912 ms (-17%)
     "abl_small": ["-DFEDMX_ABLATE=4"],            # no small-tile Adam        1.063 ms (-3%)
     "abl_adam": ["-DFEDMX_ABLATE=8"],             # no Adam at all            0.708 ms (-35%)
+    # fused verification kernel, timing-only (r2, base 24.6 us; scripts/r2_verify_ablate.sh)
+    "vabl1": ["-DFEDMX_VERIFY_ABLATE=1"],         # no forward                13.4 us
+    "vabl2": ["-DFEDMX_VERIFY_ABLATE=2"],         # no drift                  18.9 us
+    "vabl4": ["-DFEDMX_VERIFY_ABLATE=4"],         # no adoption pass          21.4 us
 }
 
 
