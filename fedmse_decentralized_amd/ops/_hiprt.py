@@ -68,6 +68,8 @@ def rt():
                 L.hipExtMallocWithFlags.restype = ctypes.c_int
                 L.hipFree.argtypes = [vp]
                 L.hipFree.restype = ctypes.c_int
+                L.hipMemcpy.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int]
+                L.hipMemcpy.restype = ctypes.c_int
                 _lib = L
     return _lib
 
@@ -142,6 +144,17 @@ class DeviceWriteBuffer:
         self.dev_ptr = p.value
         self.nbytes = nbytes
         self.np = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.host_ptr))
+        # the host's stores must reach the device copy: write a pattern, read
+        # it back through the runtime (device -> host copy), else refuse
+        pat = (np.arange(64, dtype=np.uint8) * 37 + 11).astype(np.uint8)
+        self.np[:64] = pat
+        _store_fence()()
+        back = np.zeros(64, dtype=np.uint8)
+        rc = L.hipMemcpy(back.ctypes.data, ctypes.c_void_p(self.dev_ptr), 64, 2)   # hipMemcpyDeviceToHost
+        if rc != 0 or not np.array_equal(back, pat):
+            L.hipFree(ctypes.c_void_p(self.host_ptr))
+            self.host_ptr = None
+            raise RuntimeError("host writes to fine-grained device memory are not visible to the device")
 
     def __del__(self):
         try:
@@ -203,6 +216,15 @@ class DescRing(_Ring):
             # the host's write-combined stores must be visible before the
             # launch that reads them is submitted
             self.fence = _store_fence()
+            try:
+                super().__init__(nbytes, stream)
+                return
+            except RuntimeError as e:   # no host-writable device memory here: mapped host ring
+                import logging
+
+                logging.getLogger(__name__).warning("descriptor ring in mapped host memory (%s)", e)
+                self.buffer_type = MappedBuffer
+                self.fence = None
         super().__init__(nbytes, stream)
 
     def put(self, *arrays: np.ndarray) -> List[int]:
