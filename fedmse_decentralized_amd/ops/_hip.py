@@ -266,31 +266,63 @@ def fwd_rows_per_block(total_rows: int, n_items: int) -> int:
     return int(per)
 
 
+_FWD_LAYOUTS: "OrderedDict" = None   # (x ptrs, row counts, rows per block) -> block layout (LRU)
+
+
+def _fwd_layout(x_ptrs: np.ndarray, nrows: np.ndarray, rpb: int):
+    """Block layout of a forward launch: item and first row of every block
+    (filler blocks: item -1) in dispatch order.  Cached: the vote / dev-set
+    scorings repeat the same shapes every round (building the XCD-grouped
+    order took 0.1-0.5 ms of host time per round at 8 ranks)."""
+    global _FWD_LAYOUTS
+    from collections import OrderedDict
+
+    if _FWD_LAYOUTS is None:
+        _FWD_LAYOUTS = OrderedDict()
+    key = (x_ptrs.tobytes(), nrows.tobytes(), int(rpb))
+    hit = _FWD_LAYOUTS.get(key)
+    if hit is not None:
+        _FWD_LAYOUTS.move_to_end(key)
+        return hit
+    nblk = (nrows + rpb - 1) // rpb
+    item = np.repeat(np.arange(len(nrows)), nblk)
+    first = np.repeat(np.cumsum(nblk) - nblk, nblk)
+    r0 = (np.arange(int(nblk.sum())) - first) * rpb
+    order = _xcd_order(x_ptrs[: len(nrows)], nrows, nblk)
+    if order is not None:
+        pad = order < 0
+        sel = np.where(pad, 0, order)
+        item = np.where(pad, -1, item[sel])
+        r0 = np.where(pad, 0, r0[sel])
+    layout = (item, r0)
+    _FWD_LAYOUTS[key] = layout
+    while len(_FWD_LAYOUTS) > 256:
+        _FWD_LAYOUTS.popitem(last=False)
+    return layout
+
+
 def build_fwd_desc(param_ptrs: np.ndarray, x_ptrs: np.ndarray, nrows: np.ndarray, sse_ptrs: np.ndarray,
                    lat_ptrs: np.ndarray, dims, rows_per_block: Optional[int] = None) -> np.ndarray:
     """Vectorised FwdDesc construction: split items into row blocks (the
     kernel loops over any block length in 16-row tiles)."""
     nrows = np.asarray(nrows, dtype=np.int64)
+    x_ptrs = np.asarray(x_ptrs, dtype=np.int64)
     rpb = rows_per_block or fwd_rows_per_block(int(nrows.sum()), len(nrows))
-    nblk = (nrows + rpb - 1) // rpb
-    item = np.repeat(np.arange(len(nrows)), nblk)
-    first = np.repeat(np.cumsum(nblk) - nblk, nblk)
-    r0 = (np.arange(int(nblk.sum())) - first) * rpb
+    item, r0 = _fwd_layout(x_ptrs, nrows, rpb)
+    live = item >= 0
+    it = np.where(live, item, 0)
     desc = np.zeros(len(item), dtype=FWD_DTYPE)
-    desc["params"] = param_ptrs[item]
-    desc["x"] = x_ptrs[item] + (4 * 128) * r0
-    desc["sse"] = np.where(sse_ptrs[item] != 0, sse_ptrs[item] + 4 * r0, 0)
-    desc["lat"] = np.where(lat_ptrs[item] != 0, lat_ptrs[item] + 4 * dims.latent * r0, 0)
-    desc["nrows"] = np.minimum(rpb, nrows[item] - r0)
+    desc["params"] = np.asarray(param_ptrs, dtype=np.int64)[it]
+    desc["x"] = x_ptrs[it] + (4 * 128) * r0
+    sp = np.asarray(sse_ptrs, dtype=np.int64)[it]
+    lp = np.asarray(lat_ptrs, dtype=np.int64)[it]
+    desc["sse"] = np.where(sp != 0, sp + 4 * r0, 0)
+    desc["lat"] = np.where(lp != 0, lp + 4 * dims.latent * r0, 0)
+    desc["nrows"] = np.where(live, np.minimum(rpb, nrows[it] - r0), 0)   # filler: no rows, exits at once
     desc["lat_stride"] = dims.latent
     desc["d_in"] = dims.d_in
     desc["latent"] = dims.latent
     desc["hidden"] = dims.hidden
-    order = _xcd_order(np.asarray(x_ptrs)[: len(nrows)], nrows, nblk)
-    if order is not None:
-        pad = order < 0
-        desc = desc[np.where(pad, 0, order)]
-        desc["nrows"][pad] = 0   # alignment filler: no rows, the block exits immediately
     return desc
 
 
