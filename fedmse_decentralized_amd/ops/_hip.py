@@ -279,7 +279,11 @@ def _fwd_layout(x_ptrs: np.ndarray, nrows: np.ndarray, rpb: int):
 
     if _FWD_LAYOUTS is None:
         _FWD_LAYOUTS = OrderedDict()
-    key = (x_ptrs.tobytes(), nrows.tobytes(), int(rpb))
+    # the layout depends on which items share their rows, not on the addresses
+    # (the vote data changes with every round's voter): key on the sharing
+    # pattern, items labelled by the first item with the same address
+    _, first_of, label = np.unique(x_ptrs, return_index=True, return_inverse=True)
+    key = (first_of[label].astype(np.int64).tobytes(), nrows.tobytes(), int(rpb))
     hit = _FWD_LAYOUTS.get(key)
     if hit is not None:
         _FWD_LAYOUTS.move_to_end(key)
