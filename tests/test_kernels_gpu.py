@@ -57,6 +57,31 @@ def test_forward_rows_matches_torch():
         torch.testing.assert_close(z.cpu().double(), rz, rtol=2e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("dims", [(46, 27, 7), (115, 20, 5), (120, 30, 10), (127, 27, 7)])
+def test_forward_rows_other_shapes_match_torch(dims):
+    """Shapes other than the reference's: the compact forward order (d_in <=
+    115, hidden <= 27, latent <= 7) and the identity-order fallback (wider
+    models) both match the fp64 reference, SSE and latents."""
+    from fedmse_decentralized_amd.models.layout import ModelDims
+
+    md = ModelDims(*dims)
+    params, _ = init_client_params(2, 11, md)
+    params = params + 0.05 * torch.randn(params.shape, generator=torch.Generator().manual_seed(3))
+    pad = canonical_to_padded(params, md).to(DEV)
+    g = torch.Generator().manual_seed(4)
+    xs = []
+    for n in (5, 40, 257):
+        x = torch.zeros(n, 128)
+        x[:, :md.d_in] = torch.randn(n, md.d_in, generator=g)
+        xs.append(x.to(DEV))
+    items = [(0, xs[0]), (1, xs[1]), (0, xs[2])]
+    sse, lat = _hip.forward_rows(pad, items, md, True, True)
+    for (row, x), s, z in zip(items, sse, lat):
+        rs, rz = rowwise_sse(params[row].double(), x[:, :md.d_in].cpu().double(), md)
+        torch.testing.assert_close(s.cpu().double(), rs, rtol=2e-5, atol=1e-5)
+        torch.testing.assert_close(z.cpu().double(), rz, rtol=2e-5, atol=1e-5)
+
+
 def test_weighted_sum_and_drift():
     g = torch.Generator().manual_seed(2)
     stack = canonical_to_padded(torch.randn(5, DEFAULT_DIMS.num_params, generator=g)).to(DEV)
