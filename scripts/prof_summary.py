@@ -74,9 +74,15 @@ def main(argv=None):
 def pmc_summary(db: str, kernel_substr: str = "") -> str:
     """Per-kernel PMC counter totals (and per-dispatch means) from a --pmc run."""
     c = sqlite3.connect(db)
-    rows = c.execute("select k.name, p.counter_name, sum(p.counter_value), count(distinct k.id) "
-                     "from pmc_events p join kernels k on p.event_id = k.id "
-                     "group by k.name, p.counter_name").fetchall()
+    cols = [d[0] for d in c.execute("select * from pmc_events limit 1").description or []]
+    if "dispatch_id" in cols and "name" in cols:
+        # rocpd views that carry the dispatch and kernel name on every counter row
+        rows = c.execute("select name, counter_name, sum(counter_value), count(distinct dispatch_id) "
+                         "from pmc_events group by name, counter_name").fetchall()
+    else:
+        rows = c.execute("select k.name, p.counter_name, sum(p.counter_value), count(distinct k.id) "
+                         "from pmc_events p join kernels k on p.event_id = k.id "
+                         "group by k.name, p.counter_name").fetchall()
     out = ["| kernel | counter | total | per dispatch |", "|---|---|---|---|"]
     for name, cn, v, n in sorted(rows):
         if kernel_substr and kernel_substr not in name:
