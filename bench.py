@@ -48,6 +48,8 @@ def _collectives_label(comm) -> str:
     on ROCm), gloo, or nothing (one rank: in-process loopback)."""
     if type(comm).__name__ == "PhantomComm":
         return "collectives stubbed: one-GPU projection of rank 0"
+    if getattr(comm, "active", False):
+        return "peer-memory one-shot all-gather/all-reduce (IPC over xGMI)"
     try:
         import torch.distributed as dist
 
@@ -90,6 +92,9 @@ def _main(argv, real_stdout: int):
     p.add_argument("--model-type", default="hybrid")
     p.add_argument("--update-type", default="mse_avg")
     p.add_argument("--backend", default="auto")
+    p.add_argument("--comm", default=None, choices=["rccl", "ipc"],
+                   help="N > 1: per-round collectives over RCCL (default) or one-shot peer-memory kernels "
+                        "(parallel/ipc.py); default: FEDMX_COMM or rccl")
     p.add_argument("--data-kind", default="nbaiot", choices=["nbaiot", "kitsune"],
                    help="synthetic feature family (BASELINE config 5 uses kitsune, non-IID)")
     p.add_argument("--non-iid", action="store_true", help="Dirichlet non-IID client mixtures")
@@ -115,7 +120,7 @@ def _main(argv, real_stdout: int):
 
         comm = PhantomComm(args.phantom_ranks, device)
     else:
-        comm = init_comm(device=device)
+        comm = init_comm(device=device, comm_impl=args.comm)
     setup_logging("WARNING", rank=comm.rank)
     n_gpus = comm.world_size
     if args.gpus != n_gpus and comm.is_root:

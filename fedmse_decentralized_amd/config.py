@@ -104,6 +104,11 @@ class ExperimentConfig:
     # debug: all-gather a hash of the replicated protocol state every round
     # and fail on divergence between ranks
     debug_replica_check: bool = False
+    # multi-rank transport of the device protocol's per-round collectives:
+    # "rccl" (torch.distributed: RCCL on the GPU) or "ipc" (one-shot kernels
+    # over peer-mapped memory, parallel/ipc.py; SURVEY §5.8's --comm ipc|rccl);
+    # None: FEDMX_COMM, else rccl
+    comm: Optional[str] = None
 
     # -----------------------------------------------------------------------
     @property

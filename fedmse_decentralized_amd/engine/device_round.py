@@ -177,6 +177,10 @@ class DeviceRound:
             self.xslots = fed.shard.max_local()
             self.xsend = torch.zeros(self.xslots + 1, P_PAD, dtype=f32, device=dev)
             self.xallg = torch.zeros(fed.comm.world_size * (self.xslots + 1), P_PAD, dtype=f32, device=dev)
+            if hasattr(fed.comm, "setup_exchange"):
+                # peer-memory channels (parallel/ipc.py): the gather of the
+                # exchange rows and the [AUCs | rejected] reduce; collective
+                fed.comm.setup_exchange((self.xslots + 1) * P_PAD, 4 * N)
         # verification: the aggregate on every hosted client's verification data (fixed mode: own V)
         if cfg.verification_method == "dev":
             vdata = [fed.dev_set for _ in fed.local]
@@ -420,6 +424,8 @@ class DeviceRound:
         fed = self.fed
         cfg, eng = fed.cfg, fed.engine
         rec["event"].synchronize()
+        if hasattr(fed.comm, "check"):
+            fed.comm.check()   # peer-memory exchange: no wait of this round timed out
         N = self.N
         rnd = rec["round"]
         info = log.isEnabledFor(logging.INFO)

@@ -101,6 +101,16 @@ class DecideArgs(ctypes.Structure):
 
 VERIFY_MAX_ROWS = 4096   # rows of one receiver's verification data the fused kernel keeps in LDS
 
+IPC_MAX_WORLD = 16
+IPC_MAX_CHUNKS = 64
+
+
+class IpcArgs(ctypes.Structure):
+    """fedmx_ipc.hip: one push / wait launch of the peer-memory exchange."""
+    _fields_ = [("area", ctypes.c_uint64 * IPC_MAX_WORLD), ("src", _vp), ("out", _vp), ("status", _vp),
+                ("timeout_ticks", ctypes.c_int64), ("world", _i32), ("rank", _i32), ("n_words", _i32),
+                ("slot_words", _i32), ("parity", _i32), ("seq", _i32), ("chunks", _i32), ("chunk_words", _i32)]
+
 
 class VerifyArgs(ctypes.Structure):
     _fields_ = [("D", DecideArgs), ("vx", _vp), ("vn", _vp), ("eval_params", _vp), ("best_stage", _vp),
@@ -138,6 +148,14 @@ def lib():
                 "fedmx_copy2_f64": [vp, vp, i32, vp, vp, i32, vp],
                 "fedmx_copy_rows": [vp, i32, vp, vp, i32, vp, i32, i32, vp],
                 "fedmx_protocol_sizes": [vp],
+                # one-shot peer-memory exchange (fedmx_ipc.hip, parallel/ipc.py)
+                "fedmx_ipc_alloc": [ctypes.c_size_t, ctypes.POINTER(vp), vp],
+                "fedmx_ipc_open": [vp, ctypes.POINTER(vp)],
+                "fedmx_ipc_close": [vp],
+                "fedmx_ipc_free": [vp],
+                "fedmx_ipc_push": [vp, vp],
+                "fedmx_ipc_wait_gather": [vp, vp],
+                "fedmx_ipc_wait_reduce_f64": [vp, vp],
             }
             for name, args in sig.items():
                 f = getattr(L, name)
@@ -152,6 +170,8 @@ def lib():
             L.fedmx_protocol_sizes(ctypes.cast(sz, ctypes.c_void_p))
             assert tuple(sz) == (ctypes.sizeof(ElectArgs), ctypes.sizeof(WsumArgs), ctypes.sizeof(DecideArgs),
                                  ctypes.sizeof(VerifyArgs)), tuple(sz)
+            assert L.fedmx_ipc_args_size() == ctypes.sizeof(IpcArgs)
+            assert L.fedmx_ipc_max_world() == IPC_MAX_WORLD and L.fedmx_ipc_max_chunks() == IPC_MAX_CHUNKS
             _lib = L
     return _lib
 

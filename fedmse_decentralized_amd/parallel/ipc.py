@@ -1,0 +1,258 @@
+"""One-shot peer-memory exchange: the round's collectives without RCCL.
+
+SURVEY §5.8 / §2.4 (b) ("optional C++ one-shot IPC all-gather ... benchmarked
+against RCCL and selected by ``--comm ipc|rccl``").  The reference has no
+transport at all (peers are Python objects, `src/Trainer/client_trainer.py:136-151`);
+the default multi-GPU path here is RCCL (``parallel.comm.TorchDistComm``).
+On an 8x MI355X node every GPU has a direct xGMI link to each peer and the
+per-round exchange is a few hundred KB, so a collective's cost is latency:
+RCCL's launch plus the hand-off to and from ProcessGroupNCCL's stream.
+
+``IpcComm`` keeps the torch.distributed group for bring-up, barriers and
+object exchange, and replaces the two per-round collectives of the device
+protocol (``engine/device_round.py``) with two kernel launches each on the
+caller's stream (``ops/csrc/hip/fedmx_ipc.hip``):
+
+* ``all_gather_into`` (f32 [world * rows, P], main stream): push this rank's
+  rows into every rank's receive area, then wait for every peer's flags and
+  copy the gathered block out;
+* ``all_reduce_inplace`` (f64, evaluation stream): push, then wait and sum
+  the ranks' vectors in rank order (bit-identical on every rank; each entry
+  of the protocol's vectors has one non-zero contributor, so the result
+  equals RCCL's sum exactly).
+
+Every rank allocates one receive area per channel in uncached device memory
+and exports it with ``hipIpcGetMemHandle``; the handles travel through
+``all_gather_object``; every rank opens its peers' areas.  Bring-up is
+collective and checked: allocation, opening and a self-test exchange must
+succeed on every rank, else every rank falls back to the torch.distributed
+collectives (``IpcComm.active`` False) — never a mix.  Waits are bounded
+(``FEDMX_IPC_TIMEOUT_S``, default 60 s): a peer that never arrives sets a
+host-visible status word and ``check()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+import os
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .comm import TorchDistComm
+
+log = logging.getLogger(__name__)
+
+
+class IpcUnavailable(RuntimeError):
+    pass
+
+
+class _Channel:
+    """One receive area per rank plus the sequence counter of its calls."""
+
+    def __init__(self, comm: "IpcComm", slot_words: int, chunk_target: int = 1024):
+        from ..ops import _hip
+
+        self.L = _hip.lib()
+        self.H = _hip
+        self.comm = comm
+        W, me = comm.world_size, comm.rank
+        if W > _hip.IPC_MAX_WORLD:
+            raise IpcUnavailable(f"world size {W} > {_hip.IPC_MAX_WORLD}")
+        self.world, self.rank = W, me
+        self.slot_words = (int(slot_words) + 3) & ~3
+        self.chunk_target = chunk_target
+        nbytes = 4 * (2 * W * self.slot_words + 2 * W * _hip.IPC_MAX_CHUNKS)
+        hsz = self.L.fedmx_ipc_handle_size()
+        handle = (ctypes.c_uint8 * hsz)()
+        p = ctypes.c_void_p()
+        rc = self.L.fedmx_ipc_alloc(nbytes, ctypes.byref(p), ctypes.cast(handle, ctypes.c_void_p))
+        self.own = p.value if rc == 0 else None
+        allh = comm.base_all_gather_object((rc, bytes(handle)))
+        bad = [r for r, (c, _) in enumerate(allh) if c != 0]
+        if bad:
+            self.close()
+            raise IpcUnavailable(f"receive-area allocation / export failed on ranks {bad} (codes "
+                                 f"{[allh[r][0] for r in bad]})")
+        self.opened: List[int] = []
+        areas = [0] * W
+        err = 0
+        for r, (_, h) in enumerate(allh):
+            if r == me:
+                areas[r] = self.own
+                continue
+            hb = (ctypes.c_uint8 * hsz).from_buffer_copy(h)
+            q = ctypes.c_void_p()
+            rc = self.L.fedmx_ipc_open(ctypes.cast(hb, ctypes.c_void_p), ctypes.byref(q))
+            if rc != 0 or not q.value:
+                err = rc or -1
+                break
+            areas[r] = q.value
+            self.opened.append(q.value)
+        errs = comm.base_all_gather_object(err)
+        if any(errs):
+            self.close()
+            raise IpcUnavailable(f"opening peers' receive areas failed (codes per rank {errs})")
+        self.areas = areas
+        self.seq = 0
+
+    def _args(self, src: int, out: int, n_words: int, chunks: int, chunk_words: int) -> "ctypes.Structure":
+        self.seq += 1
+        a = self.H.IpcArgs()
+        for r, v in enumerate(self.areas):
+            a.area[r] = v
+        a.src, a.out, a.status = src, out, self.comm.status_ptr
+        a.timeout_ticks = self.comm.timeout_ticks
+        a.world, a.rank, a.n_words, a.slot_words = self.world, self.rank, n_words, self.slot_words
+        a.parity, a.seq, a.chunks, a.chunk_words = self.seq & 1, self.seq, chunks, chunk_words
+        return a
+
+    def gather(self, out: torch.Tensor, t: torch.Tensor, stream: int) -> None:
+        n = t.numel()
+        chunks = max(1, min(self.H.IPC_MAX_CHUNKS, -(-n // self.chunk_target)))
+        cw = ((-(-n // chunks)) + 3) & ~3
+        a = self._args(t.data_ptr(), out.data_ptr(), n, chunks, cw)
+        self.H._check(self.L.fedmx_ipc_push(ctypes.byref(a), stream), "fedmx_ipc_push")
+        self.H._check(self.L.fedmx_ipc_wait_gather(ctypes.byref(a), stream), "fedmx_ipc_wait_gather")
+
+    def reduce_f64(self, t: torch.Tensor, stream: int) -> None:
+        n = 2 * t.numel()
+        a = self._args(t.data_ptr(), t.data_ptr(), n, 1, (n + 3) & ~3)
+        self.H._check(self.L.fedmx_ipc_push(ctypes.byref(a), stream), "fedmx_ipc_push")
+        self.H._check(self.L.fedmx_ipc_wait_reduce_f64(ctypes.byref(a), stream), "fedmx_ipc_wait_reduce_f64")
+
+    def close(self) -> None:
+        from ..ops import _hiprt
+
+        try:
+            _hiprt.device_sync()
+        except Exception:
+            pass
+        for q in getattr(self, "opened", []):
+            self.L.fedmx_ipc_close(ctypes.c_void_p(q))
+        self.opened = []
+        if getattr(self, "own", None):
+            self.L.fedmx_ipc_free(ctypes.c_void_p(self.own))
+            self.own = None
+
+
+class IpcComm(TorchDistComm):
+    """torch.distributed group + peer-memory channels for the round's
+    device-tensor collectives.  Inactive until ``setup_exchange`` succeeded
+    on every rank; calls that do not fit a channel use the base collectives."""
+
+    def __init__(self, device: Optional[torch.device] = None):
+        super().__init__(device)
+        from ..ops import _hip, _hiprt
+
+        self.active = False
+        self.ipc_calls = 0
+        self._gather: Optional[_Channel] = None
+        self._reduce: Optional[_Channel] = None
+        self._status = _hiprt.MappedBuffer(64)
+        self._status_view = self._status.view(0, np.int32, 1)
+        self._status_view[0] = 0
+        self.status_ptr = self._status.dev_ptr
+        khz = _hip.lib().fedmx_ipc_wall_khz()
+        timeout_s = float(os.environ.get("FEDMX_IPC_TIMEOUT_S", "60"))
+        self.timeout_ticks = int(timeout_s * 1e3 * (khz if khz > 0 else 100_000))
+        self._hip = _hip
+
+    # the base (torch.distributed) object exchange, also used during bring-up
+    def base_all_gather_object(self, obj):
+        return TorchDistComm.all_gather_object(self, obj)
+
+    def setup_exchange(self, gather_words: int, reduce_words: int) -> bool:
+        """Create (or keep, when large enough) the two channels; collective.
+        Returns whether the peer-memory path is active on every rank."""
+        if (self.active and self._gather.slot_words >= gather_words
+                and self._reduce.slot_words >= reduce_words):
+            return True
+        self._teardown()
+        ok, why = True, ""
+        try:
+            self._gather = _Channel(self, gather_words)
+            self._reduce = _Channel(self, reduce_words)
+            ok = self._self_test()
+            why = "self-test mismatch" if not ok else ""
+        except IpcUnavailable as e:
+            ok, why = False, str(e)
+        # every rank takes the same path
+        oks = self.base_all_gather_object(bool(ok))
+        self.active = all(oks)
+        if not self.active:
+            self._teardown()
+            if self.is_root:
+                log.warning("peer-memory exchange unavailable (%s; ranks ok: %s): using %s collectives",
+                            why or "another rank failed", oks, self.backend)
+        return self.active
+
+    def _self_test(self) -> bool:
+        """Three gathers and two reduces with rank-specific patterns (both
+        parities, reused buffers), checked on the host."""
+        dev = self.device
+        W, me = self.world_size, self.rank
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        n = min(self._gather.slot_words, 4 * 4096 + 12)
+        n -= n % 4
+        ok = True
+        for it in range(3):
+            src = (torch.arange(n, device=dev, dtype=torch.float32) * (it + 1) + 1000.0 * me)
+            out = torch.full((W, n), -1.0, device=dev, dtype=torch.float32)
+            self._gather.gather(out, src, stream)
+            exp = torch.stack([torch.arange(n, device=dev, dtype=torch.float32) * (it + 1) + 1000.0 * r
+                               for r in range(W)])
+            torch.cuda.synchronize(dev)
+            ok &= bool(torch.equal(out, exp))
+        m = min(64, self._reduce.slot_words // (2 * W))   # doubles per rank block
+        for it in range(2 if m >= 1 else 0):
+            t = torch.zeros(W * m, device=dev, dtype=torch.float64)
+            t[me * m:(me + 1) * m] = torch.arange(m, device=dev, dtype=torch.float64) + 0.5 * it + me
+            self._reduce.reduce_f64(t, stream)
+            exp = torch.cat([torch.arange(m, device=dev, dtype=torch.float64) + 0.5 * it + r for r in range(W)])
+            torch.cuda.synchronize(dev)
+            ok &= bool(torch.equal(t, exp))
+        ok &= self.status_ok()
+        return ok
+
+    def status_ok(self) -> bool:
+        return int(self._status_view[0]) == 0
+
+    def check(self) -> None:
+        """Raise if a wait timed out (a peer never arrived)."""
+        if not self.status_ok():
+            raise RuntimeError("peer-memory exchange: a wait timed out (a rank stalled or died); "
+                               "rerun with FEDMX_COMM=rccl")
+
+    def _teardown(self):
+        for ch in (self._gather, self._reduce):
+            if ch is not None:
+                ch.close()
+        self._gather = self._reduce = None
+        self.active = False
+
+    # ---- the device protocol's two collectives ------------------------------------
+    def all_gather_into(self, out, t):
+        ch = self._gather
+        if (self.active and ch is not None and t.dtype == torch.float32 and out.dtype == torch.float32
+                and t.device == self.device and out.device == self.device and t.is_contiguous()
+                and out.is_contiguous() and t.numel() % 4 == 0 and t.numel() <= ch.slot_words
+                and out.numel() == self.world_size * t.numel()):
+            ch.gather(out, t, self._hip._stream(self.device))
+            self.ipc_calls += 1
+            return
+        super().all_gather_into(out, t)
+
+    def all_reduce_inplace(self, t):
+        ch = self._reduce
+        if (self.active and ch is not None and t.dtype == torch.float64 and t.device == self.device
+                and t.is_contiguous() and 2 * t.numel() <= ch.slot_words):
+            ch.reduce_f64(t, self._hip._stream(self.device))
+            self.ipc_calls += 1
+            return
+        super().all_reduce_inplace(t)
+
+    def close(self):
+        self._teardown()

@@ -20,8 +20,18 @@ def env_world() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
-def init_comm(backend: Optional[str] = None, device: Optional[str] = None, timeout_s: int = 300) -> Comm:
-    """Create the comm for this process.  World size 1 -> LoopbackComm."""
+def init_comm(backend: Optional[str] = None, device: Optional[str] = None, timeout_s: int = 300,
+              comm_impl: Optional[str] = None) -> Comm:
+    """Create the comm for this process.  World size 1 -> LoopbackComm.
+
+    ``comm_impl`` (or ``FEDMX_COMM``): ``rccl`` (default) runs the round's
+    collectives through torch.distributed (RCCL on the GPU, gloo on the CPU);
+    ``ipc`` runs the device protocol's per-round all-gather / all-reduce as
+    one-shot peer-memory kernels (``parallel/ipc.py``), falling back to the
+    torch.distributed collectives when bring-up fails on any rank."""
+    impl = comm_impl or os.environ.get("FEDMX_COMM") or "rccl"
+    if impl not in ("rccl", "ipc"):
+        raise ValueError(f"FEDMX_COMM / --comm must be rccl or ipc, not {impl!r}")
     world = env_world()
     if device is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
@@ -58,6 +68,12 @@ def init_comm(backend: Optional[str] = None, device: Optional[str] = None, timeo
         if backend == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(**kw)
+    if impl == "ipc" and dev.type == "cuda":
+        # the round's device collectives over peer-mapped memory (parallel/ipc.py);
+        # activated collectively by the device protocol's setup_exchange
+        from .ipc import IpcComm
+
+        return IpcComm(dev)
     return TorchDistComm(dev)
 
 
@@ -65,5 +81,13 @@ def shutdown(comm: Comm) -> None:
     if isinstance(comm, TorchDistComm):
         import torch.distributed as dist
 
+        if hasattr(comm, "close"):
+            # peer-memory channels: every rank drains its queue before any
+            # area is unmapped or freed
+            if comm.device.type == "cuda":
+                torch.cuda.synchronize(comm.device)
+            comm.barrier()
+            comm.close()
+            comm.barrier()
         if dist.is_initialized():
             dist.destroy_process_group()

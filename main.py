@@ -36,7 +36,7 @@ def run_sweep(cfg: ExperimentConfig, comm=None) -> dict:
         dev = cfg.device
         if dev == "auto":
             dev = "cuda" if torch.cuda.is_available() else "cpu"
-        comm = init_comm(device=dev)
+        comm = init_comm(device=dev, comm_impl=cfg.comm)
     total = len(cfg.update_types) * len(cfg.model_types) * cfg.num_runs
     best = {mt: {ut: float("-inf") for ut in cfg.update_types} for mt in cfg.model_types}
     log.info("\n" + "=" * 50)

@@ -171,3 +171,23 @@ def test_forced_collectives_one_rank_gloo_matches_loopback(tmp_path):
                   "MASTER_PORT": str(_free_port()), "FEDMX_FORCE_COLLECTIVES": "1"}, "gloo1")
     assert forced["detection_auc_mean"] == base["detection_auc_mean"]
     assert forced["detection_auc_min"] == base["detection_auc_min"]
+
+
+def test_comm_impl_selection(monkeypatch):
+    """--comm / FEDMX_COMM: rccl or ipc only; the peer-memory path is a GPU
+    multi-rank feature (a one-rank job stays on the loopback comm)."""
+    from fedmse_decentralized_amd.config import ExperimentConfig
+    from fedmse_decentralized_amd.parallel.comm import LoopbackComm
+    from fedmse_decentralized_amd.parallel.launch import init_comm
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("FEDMX_FORCE_COLLECTIVES", raising=False)
+    with pytest.raises(ValueError):
+        init_comm(device="cpu", comm_impl="nccl2")
+    monkeypatch.setenv("FEDMX_COMM", "bogus")
+    with pytest.raises(ValueError):
+        init_comm(device="cpu")
+    monkeypatch.setenv("FEDMX_COMM", "ipc")
+    assert isinstance(init_comm(device="cpu"), LoopbackComm)
+    assert isinstance(init_comm(device="cpu", comm_impl="rccl"), LoopbackComm)
+    assert ExperimentConfig().comm is None
