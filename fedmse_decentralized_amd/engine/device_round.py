@@ -64,7 +64,6 @@ def fast_path_supported(fed) -> Optional[str]:
         (cfg.metric == "AUC", "metric is not AUC"),
         (not cfg.malicious_clients and not cfg.dropped_clients, "fault injection is enabled"),
         (not cfg.save_latents, "latent logging is enabled"),
-        (not cfg.resume and not cfg.snapshot_every, "resume snapshots are enabled"),
         (not cfg.fedavg_sample_weighted, "sample-weighted FedAvg"),
         (cfg.device_protocol, "device protocol disabled"),
     ]
@@ -202,6 +201,27 @@ class DeviceRound:
         self.host_agg_counts = [0] * N
 
     # ------------------------------------------------------------------------------
+    def snapshot(self) -> dict:
+        """The device-resident protocol state a resumed federation needs
+        (aggregation caps, every hosted receiver's verifier history and
+        rejection count); every enqueued round is collected first.  Per-round
+        scratch (vote records, election state, side-stream slots) is rewritten
+        by the next round and is not part of it."""
+        self.collect_all()
+        torch.cuda.synchronize(self.dev)
+        return {"agg_counts": self.agg_counts.cpu(), "hist": self.hist.cpu(), "has_hist": self.has_hist.cpu(),
+                "hist_perf": self.hist_perf.cpu(), "rejected": self.rejected.cpu(),
+                "host_agg_counts": torch.tensor(self.host_agg_counts, dtype=torch.int64)}
+
+    def restore(self, s: dict) -> None:
+        for k in ("agg_counts", "hist", "has_hist", "hist_perf", "rejected"):
+            t = getattr(self, k)
+            if tuple(s[k].shape) != tuple(t.shape):
+                raise ValueError(f"resume snapshot: device state {k} has shape {tuple(s[k].shape)}, "
+                                 f"this federation needs {tuple(t.shape)}")
+            t.copy_(s[k].to(t.device))
+        self.host_agg_counts = [int(x) for x in s["host_agg_counts"].tolist()]
+
     def reset_aggregation_counts(self):
         self.agg_counts.zero_()
         self.host_agg_counts = [0] * self.N

@@ -198,14 +198,17 @@ class Federation:
         if cfg.save_checkpoints:
             for d in self.save_dirs.values():
                 os.makedirs(d, exist_ok=True)
-        if cfg.resume:
-            self.restore(ckpt.load_resume(self._resume_path(cfg.resume)))
+        snap = ckpt.load_resume(self._resume_path(cfg.resume)) if cfg.resume else None
+        if snap is not None:
+            self.restore(snap)
         self._fast = None
         from .engine.device_round import DeviceRound, fast_path_supported
 
         why = fast_path_supported(self)
         if why is None:
             self._fast = DeviceRound(self)
+            if snap is not None and snap.get("device"):
+                self._fast.restore(snap["device"])
         else:
             log.debug(f"device protocol off: {why}")
         return self
@@ -586,9 +589,14 @@ class Federation:
 
     # -- resume ---------------------------------------------------------------------
     def snapshot(self) -> Dict:
+        # device-resident rounds still in flight are collected first, so the
+        # host-side state (metrics, early stop, counters) is the round's own
+        self.finish()
         st = self.engine.store
         vers = sorted(self.versions)
         return {
+            "host_noise": self.noise.get_state() if isinstance(self.noise, HostNoise) else [],
+            "device": self._fast.snapshot() if getattr(self, "_fast", None) is not None else {},
             "round_idx": self.round_idx,
             "params": st.params.cpu(), "adam_m": st.adam_m.cpu(), "adam_v": st.adam_v.cpu(),
             "adam_step": st.adam_step.cpu(), "anchor": st.anchor.cpu(), "best": st.best.cpu(),
@@ -625,6 +633,8 @@ class Federation:
         self.early.best, self.early.worse = float(s["early"][0]), int(s["early"][1])
         if s["last_metrics"].numel():
             self.last_metrics = s["last_metrics"].numpy()
+        if isinstance(self.noise, HostNoise) and s.get("host_noise"):
+            self.noise.set_state(s["host_noise"])
 
 
 _WRITER: Optional[AsyncWriter] = None

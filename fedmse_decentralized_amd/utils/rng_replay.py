@@ -89,6 +89,16 @@ class HostNoise:
     def rand(self) -> float:
         return float(self.rng.random())
 
+    def get_state(self):
+        """PCG64 state as plain ints (resume snapshots load with weights_only)."""
+        st = self.rng.bit_generator.state
+        return [int(st["state"]["state"]), int(st["state"]["inc"]), int(st["has_uint32"]), int(st["uinteger"])]
+
+    def set_state(self, s) -> None:
+        state, inc, has32, uint = (int(x) for x in s)
+        self.rng.bit_generator.state = {"bit_generator": "PCG64", "state": {"state": state, "inc": inc},
+                                        "has_uint32": has32, "uinteger": uint}
+
     def rand_n(self, n: int):
         """``n`` draws at once: the same values, in the same order, as ``n``
         calls of :meth:`rand` (one vectorised call: the k(k-1) election draws

@@ -222,3 +222,34 @@ def test_device_round_matches_host_path_large_selection(tmp_path):
     assert a["sel"] == b["sel"] and a["agg"] == b["agg"] and a["ver"] == b["ver"]
     assert torch.equal(fa.engine.store.params, fb.engine.store.params)
     assert torch.equal(fa.engine.store.anchor, fb.engine.store.anchor)
+
+
+def test_device_round_resume_matches_uninterrupted(tmp_path):
+    """Checkpoint / resume on the device-resident protocol: a
+    federation resumed from a round-3 snapshot (parameters, Adam state,
+    aggregation caps, verifier histories, tie-break noise stream) continues
+    bit-identically to the uninterrupted run."""
+    _shrink()
+    from fedmse_decentralized_amd import federation
+    from fedmse_decentralized_amd.federation import Federation
+
+    federation._PREP_CACHE.clear()
+    a = Federation(_cfg(str(tmp_path / "a"), save_checkpoints=False), "hybrid", "mse_avg", 0).setup()
+    assert a._fast is not None
+    for _ in range(3):
+        a.run_round()
+    snap = a.save_snapshot(str(tmp_path / "snap.pt"))
+    ra = [a.run_round() for _ in range(3)]
+    a.finish()
+    ra = [(r.aggregator, r.metrics.tolist(), r.verification) for r in ra]
+    federation._PREP_CACHE.clear()
+    b = Federation(_cfg(str(tmp_path / "b"), save_checkpoints=False, resume=snap), "hybrid", "mse_avg", 0).setup()
+    assert b._fast is not None and b.round_idx == 3
+    rb = [b.run_round() for _ in range(3)]
+    b.finish()
+    rb = [(r.aggregator, r.metrics.tolist(), r.verification) for r in rb]
+    assert ra == rb
+    for name in ("params", "adam_m", "adam_v", "anchor", "best"):
+        assert torch.equal(getattr(a.engine.store, name), getattr(b.engine.store, name)), name
+    for name in ("agg_counts", "hist", "has_hist", "hist_perf", "rejected"):
+        assert torch.equal(getattr(a._fast, name), getattr(b._fast, name)), name
