@@ -63,7 +63,6 @@ def fast_path_supported(fed) -> Optional[str]:
         (fed.update_type in ("avg", "fedprox", "mse_avg"), f"update type {fed.update_type}"),
         (cfg.metric == "AUC", "metric is not AUC"),
         (not cfg.malicious_clients and not cfg.dropped_clients, "fault injection is enabled"),
-        (not cfg.save_latents, "latent logging is enabled"),
         (not cfg.fedavg_sample_weighted, "sample-weighted FedAvg"),
         (cfg.device_protocol, "device protocol disabled"),
     ]
@@ -403,6 +402,7 @@ class DeviceRound:
                                0, 0, 0, dev)
                 rec["snap_slot"] = si
             eng.evaluate_launch(fed.model_type, params=eval_params)
+            rec["eval_params"] = eval_params   # --save-latents: the plan whose latent buffers hold this round's
             aucs_ptr = eng._plan(fed.model_type, eval_params)["aucs_buf"].dev_ptr
             if not comm.collective:
                 _hip.copy2_f64(slot_ptr, aucs_ptr, N, slot_ptr + 8 * N, side_rep.data_ptr() + 8 * N, N, dev)
@@ -497,6 +497,15 @@ class DeviceRound:
             m_ = metrics.copy()
             fed.writer.submit(lambda m_=m_, rnd=rnd: fed._report_round(rnd, m_))
         fed.last_metrics = metrics
+        if cfg.save_latents and fed.model_type == "hybrid" and fed.local:
+            # LatentData pickles: every hosted client's test-set
+            # latents of this round's evaluation.  The side slot's plan is not
+            # reused before this round is collected (NSIDE > max_pending).
+            p = eng._plan(fed.model_type, rec["eval_params"])
+            st = eng.store
+            fed.latent_log[rnd] = {fed.clients[c].name: (l.detach().cpu().numpy().astype(np.float32),
+                                                         st.labels(i).astype(np.float32))
+                                   for i, (c, l) in enumerate(zip(fed.local, p["test_lat"]))}
         if cfg.debug_replica_check:
             fed.check_replicas(rnd, rec["selected"], aggregator, metrics)
         stop = False
@@ -504,6 +513,6 @@ class DeviceRound:
             stop = fed.early.update(float(np.min(metrics)))
         rec.update(aggregator=aggregator, metrics=metrics, verification=verification, epochs_run=epochs_local,
                    stop=stop, done=True)
-        for key in ("handle", "snap_slot", "slot", "report", "_keep", "event"):
+        for key in ("handle", "snap_slot", "slot", "report", "_keep", "event", "eval_params"):
             rec.pop(key, None)
         self.all_rounds.pop(rnd, None)

@@ -253,3 +253,21 @@ def test_device_round_resume_matches_uninterrupted(tmp_path):
         assert torch.equal(getattr(a.engine.store, name), getattr(b.engine.store, name)), name
     for name in ("agg_counts", "hist", "has_hist", "hist_perf", "rejected"):
         assert torch.equal(getattr(a._fast, name), getattr(b._fast, name)), name
+
+
+def test_device_round_save_latents_matches_host_path(tmp_path):
+    """--save-latents (LatentData pickles) on the device-resident
+    protocol: the same per-round test-set latents as the host path."""
+    _shrink()
+    fa, _ = _run(_cfg(str(tmp_path / "dev"), save_checkpoints=False, save_latents=True), "mse_avg", 4)
+    fb, _ = _run(_cfg(str(tmp_path / "host"), save_checkpoints=False, save_latents=True, device_protocol=False),
+                 "mse_avg", 4)
+    assert fa._fast is not None and fb._fast is None
+    assert sorted(fa.latent_log) == sorted(fb.latent_log) == [0, 1, 2, 3]
+    for r in fa.latent_log:
+        assert sorted(fa.latent_log[r]) == sorted(fb.latent_log[r])
+        for name, (lat, lab) in fa.latent_log[r].items():
+            lat_b, lab_b = fb.latent_log[r][name]
+            assert lat.shape[1] == 7
+            np.testing.assert_array_equal(lat, lat_b)
+            np.testing.assert_array_equal(lab, lab_b)
