@@ -160,7 +160,7 @@ def add_arguments(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
         if isinstance(default, bool):
             p.add_argument(name, type=_str2bool, default=None, metavar="BOOL")
         elif isinstance(default, list):
-            elem = int if f.name == "malicious_clients" else str
+            elem = int if f.name in ("malicious_clients", "dropped_clients") else str
             p.add_argument(name, type=elem, nargs="*", default=None)
         elif isinstance(default, int) and not isinstance(default, bool):
             p.add_argument(name, type=int, default=None)

@@ -62,7 +62,10 @@ def fast_path_supported(fed) -> Optional[str]:
         (cfg.protocol_variant == "code", "protocol variant is not 'code'"),
         (fed.update_type in ("avg", "fedprox", "mse_avg"), f"update type {fed.update_type}"),
         (cfg.metric == "AUC", "metric is not AUC"),
-        (not cfg.malicious_clients and not cfg.dropped_clients, "fault injection is enabled"),
+        # dropped clients leave at least one selection per round (k >= 1: the
+        # election kernel needs a voter); larger drop sets take the host path
+        (len({c for c in cfg.dropped_clients if 0 <= c < fed.N}) < max(1, int(cfg.num_participants * fed.N)),
+         "fault injection could drop every selected client"),
         (not cfg.fedavg_sample_weighted, "sample-weighted FedAvg"),
         (cfg.device_protocol, "device protocol disabled"),
     ]
@@ -258,6 +261,9 @@ class DeviceRound:
         with tel.phase("train"):
             handle = eng.train_launch(local_rows, fed.hp) if local_sel else None
             rec["handle"] = handle
+            for c in local_sel:
+                if c in cfg.malicious_clients:   # fault injection: poisoned update (stream-ordered)
+                    st.params[self._loc(c)].mul_(cfg.malicious_scale)
         with tel.phase("vote"):
             if local_sel:
                 if ev_std is not None:

@@ -271,3 +271,21 @@ def test_device_round_save_latents_matches_host_path(tmp_path):
             assert lat.shape[1] == 7
             np.testing.assert_array_equal(lat, lat_b)
             np.testing.assert_array_equal(lab, lab_b)
+
+
+def test_device_round_fault_injection_matches_host_path(tmp_path):
+    """Fault injection on the device-resident protocol: a dropped client
+    never trains, votes or aggregates, a malicious client's poisoned update
+    is screened by the verifiers — decisions, counts and parameters equal the
+    host path's."""
+    _shrink()
+    kw = dict(save_checkpoints=False, dropped_clients=[1], malicious_clients=[2], malicious_scale=25.0)
+    fa, a = _run(_cfg(str(tmp_path / "dev"), **kw), "mse_avg", 6)
+    fb, b = _run(_cfg(str(tmp_path / "host"), device_protocol=False, **kw), "mse_avg", 6)
+    assert fa._fast is not None and fb._fast is None
+    assert all(1 not in s for s in a["sel"])
+    assert a["sel"] == b["sel"] and a["agg"] == b["agg"] and a["ver"] == b["ver"]
+    for x, y in zip(a["metrics"], b["metrics"]):
+        np.testing.assert_array_equal(np.array(x), np.array(y))
+    assert torch.equal(fa.engine.store.params, fb.engine.store.params)
+    assert fa.agg_counts == fb.agg_counts

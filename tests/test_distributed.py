@@ -191,3 +191,14 @@ def test_comm_impl_selection(monkeypatch):
     assert isinstance(init_comm(device="cpu"), LoopbackComm)
     assert isinstance(init_comm(device="cpu", comm_impl="rccl"), LoopbackComm)
     assert ExperimentConfig().comm is None
+
+
+def test_fault_injection_cli_lists_are_ints():
+    import argparse
+
+    from fedmse_decentralized_amd.config import add_arguments, from_args
+
+    ns = add_arguments(argparse.ArgumentParser()).parse_args(["--dropped-clients", "1", "3",
+                                                              "--malicious-clients", "2"])
+    cfg = from_args(ns)
+    assert cfg.dropped_clients == [1, 3] and cfg.malicious_clients == [2]
