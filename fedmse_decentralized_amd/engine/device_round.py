@@ -66,7 +66,6 @@ def fast_path_supported(fed) -> Optional[str]:
         # election kernel needs a voter); larger drop sets take the host path
         (len({c for c in cfg.dropped_clients if 0 <= c < fed.N}) < max(1, int(cfg.num_participants * fed.N)),
          "fault injection could drop every selected client"),
-        (not cfg.fedavg_sample_weighted, "sample-weighted FedAvg"),
         (cfg.device_protocol, "device protocol disabled"),
     ]
     for ok, why in checks:
@@ -197,7 +196,10 @@ class DeviceRound:
             self._vdata = vdata
             self.vx = torch.tensor([d.data_ptr() for d in vdata], dtype=torch.int64, device=dev)
         self.fused_verify = bool(fed.local) and max(int(d.shape[0]) for d in vdata) <= _hip.VERIFY_MAX_ROWS
-        self.rule = 1 if fed.update_type == "mse_avg" else 0
+        # aggregation weights: 1 = FedMSE 1/MSE (device), 0 = plain mean,
+        # 2 = sample-weighted FedAvg (host-computed: they depend on the selection only)
+        self.rule = 1 if fed.update_type == "mse_avg" else (2 if cfg.fedavg_sample_weighted else 0)
+        self.n_train = {c: fed.clients[c].train.shape[0] for c in range(N)}
         self.pending: deque = deque()
         self.all_rounds: Dict[int, dict] = {}
         self.host_agg_counts = [0] * N
@@ -342,12 +344,18 @@ class DeviceRound:
                 sel_ptr, noise_ptr, rows_ptr = self.rt.desc.put(np.asarray(selected, dtype=np.int32),
                                                                 noise if noise.size else np.zeros(1), rows)
                 rec_ptr, vec_ptr = 0, self.vec.data_ptr()
+            hw_ptr = 0
+            if self.rule == 2:
+                from ..protocol.aggregation import plan_mean
+
+                (hw_ptr,) = self.rt.desc.put(np.asarray([w for _, w in plan_mean(selected, self.n_train)],
+                                                        dtype=np.float32))
             rep_ptr, rep_view = self.rt.out.take(np.int32, 2)
             rep_view[:] = -2
             a = _hip.ElectArgs(sel=sel_ptr, vec=vec_ptr, noise=noise_ptr,
                                agg_counts=self.agg_counts.data_ptr(), weights=self.weights.data_ptr(),
                                state=self.state.data_ptr(), report=rep_ptr, k=k, cap=cfg.max_aggregation,
-                               rule=self.rule, pad=0, rec=rec_ptr)
+                               rule=self.rule, pad=0, rec=rec_ptr, hw=hw_ptr)
             w = _hip.WsumArgs(base=base.data_ptr(), rows=rows_ptr, weights=self.weights.data_ptr(),
                               state=self.state.data_ptr(), out=self.agg.data_ptr(), k=k, P=P_PAD)
             _hip.elect_wsum(a, w, dev)

@@ -37,12 +37,14 @@ struct ElectArgs {
   float* weights;          // [k] out
   int32_t* state;          // [4] out: aggregator (-1: none), voter
   int32_t* report;         // [2] out (mapped host memory): aggregator, voter
-  int32_t k, cap, rule;    // rule 0: mean (avg / fedprox), 1: 1/MSE (mse_avg)
+  int32_t k, cap, rule;    // rule 0: mean (avg / fedprox), 1: 1/MSE (mse_avg),
+                           // 2: host-computed weights hw (sample-weighted FedAvg)
   int32_t pad;
   const int32_t* rec;      // [k] record index (4-double units into vec) of each selection, or
                            // null: the client id (multi-rank: records read in place from the exchange buffer)
+  const float* hw;         // rule 2: [k] weights (they depend on the selection only)
 };
-static_assert(sizeof(ElectArgs) == 80, "ElectArgs layout is shared with Python");
+static_assert(sizeof(ElectArgs) == 88, "ElectArgs layout is shared with Python");
 
 struct WsumArgs {
   const float* base;       // row-major [*, P]
@@ -126,6 +128,8 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
           double tot = 0.0;
           for (int j = 0; j < k; ++j) tot += s_inv[j];   // selection order, as the serial form
           if (lane < k) s_w[lane] = (float)(s_inv[lane] / tot);
+        } else if (E.rule == 2) {
+          if (lane < k) s_w[lane] = E.hw[lane];
         } else if (lane < k) {
           s_w[lane] = (float)(1.0 / (double)k);
         }
@@ -167,6 +171,8 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
         for (int j = 0; j < E.k; ++j) tot += 1.0 / E.vec[(size_t)(E.rec != nullptr ? E.rec[j] : E.sel[j]) * 4 + 3];
         for (int j = 0; j < E.k; ++j)
           s_w[j] = (float)((1.0 / E.vec[(size_t)(E.rec != nullptr ? E.rec[j] : E.sel[j]) * 4 + 3]) / tot);
+      } else if (E.rule == 2) {
+        for (int j = 0; j < E.k; ++j) s_w[j] = E.hw[j];
       } else {
         const float w = (float)(1.0 / (double)E.k);
         for (int j = 0; j < E.k; ++j) s_w[j] = w;

@@ -156,8 +156,8 @@ class IpcComm(TorchDistComm):
         self._status_view[0] = 0
         self.status_ptr = self._status.dev_ptr
         khz = _hip.lib().fedmx_ipc_wall_khz()
-        timeout_s = float(os.environ.get("FEDMX_IPC_TIMEOUT_S", "60"))
-        self.timeout_ticks = int(timeout_s * 1e3 * (khz if khz > 0 else 100_000))
+        self._timeout_s = float(os.environ.get("FEDMX_IPC_TIMEOUT_S", "60"))
+        self.timeout_ticks = int(self._timeout_s * 1e3 * (khz if khz > 0 else 100_000))
         self._hip = _hip
 
     # the base (torch.distributed) object exchange, also used during bring-up
@@ -175,10 +175,22 @@ class IpcComm(TorchDistComm):
         try:
             self._gather = _Channel(self, gather_words)
             self._reduce = _Channel(self, reduce_words)
-            ok = self._self_test()
-            why = "self-test mismatch" if not ok else ""
-        except IpcUnavailable as e:
+        except IpcUnavailable as e:   # raised collectively: every rank saw the same codes
             ok, why = False, str(e)
+        if ok:
+            # a rank whose self-test fails (a launch error, a mismatch or a peer
+            # that never arrives: the waits are bounded by a short timeout here)
+            # still reaches the agreement below
+            full = self.timeout_ticks
+            self.timeout_ticks = max(1, full * 10 // max(1, int(self._timeout_s)))
+            try:
+                ok = self._self_test()
+                why = "self-test mismatch or timeout" if not ok else ""
+            except Exception as e:   # noqa: BLE001 - any local failure means: not on this rank
+                ok, why = False, f"self-test failed: {e}"
+            finally:
+                self.timeout_ticks = full
+                self._status_view[0] = 0
         # every rank takes the same path
         oks = self.base_all_gather_object(bool(ok))
         self.active = all(oks)

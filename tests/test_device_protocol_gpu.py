@@ -289,3 +289,19 @@ def test_device_round_fault_injection_matches_host_path(tmp_path):
         np.testing.assert_array_equal(np.array(x), np.array(y))
     assert torch.equal(fa.engine.store.params, fb.engine.store.params)
     assert fa.agg_counts == fb.agg_counts
+
+
+def test_device_round_sample_weighted_fedavg_matches_host_path(tmp_path):
+    """Sample-weighted FedAvg (weights ∝ training-set size) on the device
+    protocol (host-computed weights, rule 2 of the election kernel): the same
+    aggregates as the host path's weighted_sum."""
+    _shrink()
+    fa, a = _run(_cfg(str(tmp_path / "dev"), save_checkpoints=False, fedavg_sample_weighted=True), "avg", 4)
+    fb, b = _run(_cfg(str(tmp_path / "host"), save_checkpoints=False, fedavg_sample_weighted=True,
+                      device_protocol=False), "avg", 4)
+    fc, c = _run(_cfg(str(tmp_path / "mean"), save_checkpoints=False), "avg", 4)
+    assert fa._fast is not None and fa._fast.rule == 2 and fb._fast is None
+    assert a["sel"] == b["sel"] and a["agg"] == b["agg"] and a["ver"] == b["ver"]
+    assert torch.equal(fa.engine.store.params, fb.engine.store.params)
+    # and the weighting is not the plain mean's
+    assert not torch.equal(fa.engine.store.params, fc.engine.store.params)
