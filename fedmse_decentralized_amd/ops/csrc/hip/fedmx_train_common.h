@@ -318,6 +318,30 @@ __device__ __forceinline__ float* master_slot(int e, int i, float* sW1, float* s
   return &sW4[(q / HP) * S_W4 + hpos_of_storage<CP>(q % HP + i)];
 }
 
+// a staging thread's share of one padded parameter-sized tensor (the load
+// half of global_to_masters_o: a kernel can issue several tensors' loads in
+// one memory round trip, then write them to the masters one at a time)
+__device__ __forceinline__ void stage_load(const float* __restrict__ src, f32x4 (&val)[STAGE_PER_THREAD]) {
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
+#pragma unroll
+  for (int k = 0; k < STAGE_PER_THREAD; ++k) val[k] = s4[threadIdx.x + 256 * k];
+}
+
+template <bool CP>
+__device__ __forceinline__ void vals_to_masters_o(const f32x4 (&val)[STAGE_PER_THREAD], float* sW1, float* sW4,
+                                                  float* sW2, float* sW3) {
+#pragma unroll
+  for (int k = 0; k < STAGE_PER_THREAD; ++k) {
+    const int e = 4 * (threadIdx.x + 256 * k);
+    if (e < OFF_W2 || !CP) {   // rows permuted at most: one float4
+      lds_write4(master_slot<CP>(e, 0, sW1, sW4, sW2, sW3), val[k]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *master_slot<CP>(e, i, sW1, sW4, sW2, sW3) = val[k][i];
+    }
+  }
+}
+
 template <bool CP>
 __device__ __forceinline__ void global_to_masters_o(const float* __restrict__ src, float* sW1, float* sW4,
                                                     float* sW2, float* sW3) {

@@ -432,8 +432,18 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     __syncthreads();   // sLoss reuse / masters stable for the snapshot copy
     return worse >= A.patience && worse > 0;
   };
-  auto stage = [&](const float* src) {
-    if (stager) global_to_masters_o<CP>(src, sW1, sW4, sW2, sW3);
+  // prologue staging: the stagers issue the loads of every state tensor
+  // (m, v, [anchor], params) in one memory round trip, then each tensor
+  // passes through the masters in turn (the barrier sequence of one global_to_masters_o pass per tensor)
+  f32x4 pv_m[STAGE_PER_THREAD], pv_v[STAGE_PER_THREAD], pv_a[STAGE_PER_THREAD], pv_p[STAGE_PER_THREAD];
+  if (stager) {
+    stage_load(Mg, pv_m);
+    stage_load(Vg, pv_v);
+    if (PROX) stage_load(A.anchor + (size_t)cid * P_PAD, pv_a);
+    stage_load(Pg, pv_p);
+  }
+  auto stage_vals = [&](const f32x4 (&v)[STAGE_PER_THREAD]) {
+    if (stager) vals_to_masters_o<CP>(v, sW1, sW4, sW2, sW3);
     __syncthreads();
   };
 
@@ -441,18 +451,18 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     // =========================== helper waves ===================================
     if (FEDMX_HW_PRIO) __builtin_amdgcn_s_setprio(0);
     HSlab P4, M4, V4, AN4;
-    stage(Mg);
+    stage_vals(pv_m);
     lds_to_hslab(M4, L);
     __syncthreads();
-    stage(Vg);
+    stage_vals(pv_v);
     lds_to_hslab(V4, L);
     __syncthreads();
     if (PROX) {
-      stage(A.anchor + (size_t)cid * P_PAD);
+      stage_vals(pv_a);
       lds_to_hslab(AN4, L);
       __syncthreads();
     }
-    stage(Pg);
+    stage_vals(pv_p);
     lds_to_hslab(P4, L);
     auto publish_q4 = [&]() {
 #pragma unroll
@@ -540,18 +550,18 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // (FEDMX_HW_PRIO: the chain's wave wins issue arbitration against its helper)
   if (FEDMX_HW_PRIO) __builtin_amdgcn_s_setprio(FEDMX_HW_PRIO);
   MSlab P, M, V, AN;
-  stage(Mg);
+  stage_vals(pv_m);
   lds_to_mslab(M, L);
   __syncthreads();
-  stage(Vg);
+  stage_vals(pv_v);
   lds_to_mslab(V, L);
   __syncthreads();
   if (PROX) {
-    stage(A.anchor + (size_t)cid * P_PAD);
+    stage_vals(pv_a);
     lds_to_mslab(AN, L);
     __syncthreads();
   }
-  stage(Pg);
+  stage_vals(pv_p);
   lds_to_mslab(P, L);   // W2/W3/W4 masters stay live; W1 lives in registers only
 
   auto l1_partial = [&](const XChunk& x, f32x4& acc0, f32x4& acc1) {
