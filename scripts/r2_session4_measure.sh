@@ -5,7 +5,7 @@ set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-O=gpurun_out/s4
+O=gpurun_out/${MEASURE_DIR:-s4}
 mkdir -p $O
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 250 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; tail -n 2 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
