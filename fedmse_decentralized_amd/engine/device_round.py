@@ -57,8 +57,8 @@ def fast_path_supported(fed) -> Optional[str]:
         return "engine is not the HIP engine"
     checks = [
         (cfg.compat == "fixed", "compat mode is not 'fixed'"),
-        (cfg.election == "first_voter", "election is not first_voter"),
-        (cfg.aggregation_mode == "decentralized", "aggregation mode is not decentralized"),
+        (cfg.election in ("first_voter", "majority"), f"election {cfg.election}"),
+        (cfg.aggregation_mode in ("decentralized", "centralized"), f"aggregation mode {cfg.aggregation_mode}"),
         (cfg.protocol_variant == "code", "protocol variant is not 'code'"),
         (fed.update_type in ("avg", "fedprox", "mse_avg"), f"update type {fed.update_type}"),
         (cfg.metric == "AUC", "metric is not AUC"),
@@ -200,6 +200,10 @@ class DeviceRound:
         # 2 = sample-weighted FedAvg (host-computed: they depend on the selection only)
         self.rule = 1 if fed.update_type == "mse_avg" else (2 if cfg.fedavg_sample_weighted else 0)
         self.n_train = {c: fed.clients[c].train.shape[0] for c in range(N)}
+        # protocol variants the kernels implement: majority election (every
+        # selected client votes) and the centralised push (no verification)
+        self.elect_mode = 1 if cfg.election == "majority" else 0
+        self.centralized = cfg.aggregation_mode == "centralized"
         self.pending: deque = deque()
         self.all_rounds: Dict[int, dict] = {}
         self.host_agg_counts = [0] * N
@@ -355,7 +359,7 @@ class DeviceRound:
             a = _hip.ElectArgs(sel=sel_ptr, vec=vec_ptr, noise=noise_ptr,
                                agg_counts=self.agg_counts.data_ptr(), weights=self.weights.data_ptr(),
                                state=self.state.data_ptr(), report=rep_ptr, k=k, cap=cfg.max_aggregation,
-                               rule=self.rule, pad=0, rec=rec_ptr, hw=hw_ptr)
+                               rule=self.rule, mode=self.elect_mode, rec=rec_ptr, hw=hw_ptr)
             w = _hip.WsumArgs(base=base.data_ptr(), rows=rows_ptr, weights=self.weights.data_ptr(),
                               state=self.state.data_ptr(), out=self.agg.data_ptr(), k=k, P=P_PAD)
             _hip.elect_wsum(a, w, dev)
@@ -381,7 +385,8 @@ class DeviceRound:
                                 has_hist=self.has_hist.data_ptr(), hist_perf=self.hist_perf.data_ptr(),
                                 rejected=self.rejected.data_ptr(), rej_out=side_rep.data_ptr() + 8 * N,
                                 thr=float(cfg.verification_threshold), pthr=float(cfg.performance_threshold),
-                                start=self.start, n_local=self.n_local, P=P_PAD, d_in=fed.dims.d_in)
+                                start=self.start, n_local=self.n_local, P=P_PAD, d_in=fed.dims.d_in,
+                                mode=1 if self.centralized else 0, pad=0)
             if self.fused_verify:
                 # verification forward, decisions, adoption and the evaluation /
                 # artefact snapshots in one launch (bit-identical to the
@@ -490,7 +495,13 @@ class DeviceRound:
                     [bool(res.best_epoch[i] >= 0) for i in range(len(sel))],
                     [list(res.tracking[i]) for i in range(len(sel))])
         verification = []
-        if aggregator is not None:
+        if aggregator is not None and self.centralized:
+            # centralised push: every client adopted the aggregate, nothing to report
+            self.host_agg_counts[aggregator] += 1
+            fed.agg_counts[aggregator] += 1
+            if info:
+                log.info(f"Client {aggregator + 1} selected as aggregator")
+        elif aggregator is not None:
             self.host_agg_counts[aggregator] += 1
             fed.agg_counts[aggregator] += 1
             if info:

@@ -84,7 +84,7 @@ _vp, _i32 = ctypes.c_void_p, ctypes.c_int32
 
 class ElectArgs(ctypes.Structure):
     _fields_ = [("sel", _vp), ("vec", _vp), ("noise", _vp), ("agg_counts", _vp), ("weights", _vp), ("state", _vp),
-                ("report", _vp), ("k", _i32), ("cap", _i32), ("rule", _i32), ("pad", _i32), ("rec", _vp),
+                ("report", _vp), ("k", _i32), ("cap", _i32), ("rule", _i32), ("mode", _i32), ("rec", _vp),
                 ("hw", _vp)]
 
 
@@ -97,7 +97,7 @@ class DecideArgs(ctypes.Structure):
                 ("sse_off", _vp), ("sse_n", _vp), ("seg", _vp), ("agg_counts", _vp), ("has_hist", _vp),
                 ("hist_perf", _vp), ("rejected", _vp), ("rej_out", _vp),
                 ("thr", ctypes.c_double), ("pthr", ctypes.c_double), ("start", _i32), ("n_local", _i32),
-                ("P", _i32), ("d_in", _i32)]
+                ("P", _i32), ("d_in", _i32), ("mode", _i32), ("pad", _i32)]
 
 
 VERIFY_MAX_ROWS = 4096   # rows of one receiver's verification data the fused kernel keeps in LDS

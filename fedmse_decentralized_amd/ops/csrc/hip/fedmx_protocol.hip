@@ -39,7 +39,9 @@ struct ElectArgs {
   int32_t* report;         // [2] out (mapped host memory): aggregator, voter
   int32_t k, cap, rule;    // rule 0: mean (avg / fedprox), 1: 1/MSE (mse_avg),
                            // 2: host-computed weights hw (sample-weighted FedAvg)
-  int32_t pad;
+  int32_t mode;            // 0: first voter decides (client_trainer.py:249-285 + main.py:284-288);
+                           // 1: majority of every selected voter's ballot (legacy
+                           //    GlobalAggregator.select_aggregator; ties: selection order)
   const int32_t* rec;      // [k] record index (4-double units into vec) of each selection, or
                            // null: the client id (multi-rank: records read in place from the exchange buffer)
   const float* hw;         // rule 2: [k] weights (they depend on the selection only)
@@ -92,7 +94,8 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
         cnt = E.agg_counts[c];
       }
       int agg = -1, voter = -1;
-      for (int vi = 0; vi < k && agg < 0; ++vi) {
+      int my_votes = 0;   // majority: ballots naming this lane's client
+      for (int vi = 0; vi < k && (agg < 0 || E.mode == 1); ++vi) {
         const int v = __shfl(c, vi, 64);
         // candidate lane ci != vi draws noise entry j = ci - (ci > vi)
         bool cand = lane < k && lane != vi && cnt < E.cap;
@@ -116,7 +119,21 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
         if (best >= 0) {
           agg = __shfl(c, best, 64);
           voter = v;
+          if (lane == best) ++my_votes;
         }
+      }
+      if (E.mode == 1) {
+        // most ballots wins, ties to the earliest in selection order
+        int top = -1, top_votes = 0;
+        for (int ci = 0; ci < k; ++ci) {
+          const int vc = __shfl(my_votes, ci, 64);
+          if (vc > top_votes) {
+            top = ci;
+            top_votes = vc;
+          }
+        }
+        agg = top >= 0 ? __shfl(c, top, 64) : -1;
+        voter = -1;
       }
       if (lane == 0) s_agg = agg;
       if (agg >= 0) {
@@ -144,10 +161,13 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
     }
   } else if (tid == 0) {
     int agg = -1, voter = -1;
-    for (int vi = 0; vi < E.k && agg < 0; ++vi) {
+    int* s_votes = reinterpret_cast<int*>(s_w);   // majority tally (s_w is written after it)
+    if (E.mode == 1)
+      for (int j = 0; j < E.k; ++j) s_votes[j] = 0;
+    for (int vi = 0; vi < E.k && (agg < 0 || E.mode == 1); ++vi) {
       const int v = E.sel[vi];
       const double* u = E.noise + (size_t)vi * (E.k - 1);
-      int best = -1, j = 0;
+      int best = -1, best_ci = -1, j = 0;
       double best_s = 0.0;
       for (int ci = 0; ci < E.k; ++ci) {
         const int c = E.sel[ci];
@@ -156,13 +176,25 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
         const double sc = E.vec[(size_t)(E.rec != nullptr ? E.rec[ci] : c) * 4] * f;
         if (E.agg_counts[c] < E.cap && (best < 0 || sc < best_s)) {
           best = c;
+          best_ci = ci;
           best_s = sc;
         }
       }
       if (best >= 0) {
         agg = best;
         voter = v;
+        if (E.mode == 1) ++s_votes[best_ci];
       }
+    }
+    if (E.mode == 1) {
+      int top = -1, top_votes = 0;
+      for (int ci = 0; ci < E.k; ++ci)
+        if (s_votes[ci] > top_votes) {
+          top = ci;
+          top_votes = s_votes[ci];
+        }
+      agg = top >= 0 ? E.sel[top] : -1;
+      voter = -1;
     }
     s_agg = agg;
     if (agg >= 0) {
@@ -252,8 +284,12 @@ struct DecideArgs {
   double* rej_out;         // [N] rejected count per receiver (global id)
   double thr, pthr;
   int32_t start, n_local, P, d_in;
+  int32_t mode;            // 0: receivers verify (ModelVerifier); 1: centralised push (legacy
+                           //    GlobalAggregator.update): every hosted client, the aggregator
+                           //    included, loads the aggregate and re-anchors FedProx, no verification
+  int32_t pad;
 };
-static_assert(sizeof(DecideArgs) == 144, "DecideArgs layout is shared with Python");
+static_assert(sizeof(DecideArgs) == 152, "DecideArgs layout is shared with Python");
 
 // One 1024-thread workgroup per hosted client.  The verification MSE and the
 // parameter drift are reduced here with exactly the arithmetic of
@@ -273,6 +309,13 @@ __global__ __launch_bounds__(1024) void decide_adopt_kernel(const DecideArgs A) 
   const size_t off = (size_t)cl * A.P;
   const f32x4* src = reinterpret_cast<const f32x4*>(A.agg);
   const int n4 = A.P / 4;
+  if (A.mode == 1) {  // centralised push: load + re-anchor, nothing verified
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+      reinterpret_cast<f32x4*>(A.params + off)[i] = src[i];
+      reinterpret_cast<f32x4*>(A.anchor + off)[i] = src[i];
+    }
+    return;
+  }
   if (c == a) {  // the aggregator loads its aggregate (anchor unchanged)
     for (int i = threadIdx.x; i < n4; i += blockDim.x) reinterpret_cast<f32x4*>(A.params + off)[i] = src[i];
     return;
@@ -406,7 +449,9 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
   f32x4* bst = reinterpret_cast<f32x4*>(V.best_stage + off);
   const f32x4* bsrc = reinterpret_cast<const f32x4*>(V.best + off);
   bool ok = false, load = false;
-  if (a >= 0 && c == a) {
+  if (a >= 0 && A.mode == 1) {
+    load = ok = true;   // centralised push: every hosted client loads and re-anchors
+  } else if (a >= 0 && c == a) {
     load = true;   // the aggregator loads its aggregate (anchor / history unchanged)
   } else if (a >= 0) {
     const int had_hist = A.has_hist[cl];
@@ -513,7 +558,7 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
   }
   // ---- adoption + history + snapshots in one pass over the row
   if (FEDMX_VERIFY_ABLATE & 4) return;
-  const bool receiver = a >= 0 && c != a;
+  const bool receiver = a >= 0 && c != a && A.mode == 0;
   constexpr int UA = (P_PAD / 4 + 511) / 512;   // every element of the row in one pass of loads
   f32x4 v[UA], pv[UA], bv[UA];
 #pragma unroll

@@ -305,3 +305,27 @@ def test_device_round_sample_weighted_fedavg_matches_host_path(tmp_path):
     assert torch.equal(fa.engine.store.params, fb.engine.store.params)
     # and the weighting is not the plain mean's
     assert not torch.equal(fa.engine.store.params, fc.engine.store.params)
+
+
+@pytest.mark.parametrize("election,mode,n", [("majority", "decentralized", 6), ("first_voter", "centralized", 6),
+                                              ("majority", "centralized", 6), ("majority", "decentralized", 132)])
+def test_device_round_protocol_variants_match_host_path(tmp_path, election, mode, n):
+    """The legacy centralised GlobalAggregator variants on the
+    device protocol: majority election (every selected client votes; the
+    k > 64 case takes the election kernel's serial path) and the centralised
+    push (every client adopts and re-anchors, nothing verified) match the
+    host-decision path."""
+    _shrink()
+    kw = dict(save_checkpoints=False, election=election, aggregation_mode=mode, network_size=n)
+    rounds = 4 if n < 100 else 2
+    fa, a = _run(_cfg(str(tmp_path / "dev"), **kw), "mse_avg", rounds)
+    fb, b = _run(_cfg(str(tmp_path / "host"), device_protocol=False, **kw), "mse_avg", rounds)
+    assert fa._fast is not None and fb._fast is None
+    assert a["sel"] == b["sel"] and a["agg"] == b["agg"] and a["ver"] == b["ver"]
+    for x, y in zip(a["metrics"], b["metrics"]):
+        np.testing.assert_array_equal(np.array(x), np.array(y))
+    assert torch.equal(fa.engine.store.params, fb.engine.store.params)
+    assert torch.equal(fa.engine.store.anchor, fb.engine.store.anchor)
+    assert fa.agg_counts == fb.agg_counts
+    if mode == "centralized":
+        assert all(v == [] for v in a["ver"])
