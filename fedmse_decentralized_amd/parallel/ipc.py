@@ -260,7 +260,7 @@ class IpcComm(TorchDistComm):
     def all_reduce_inplace(self, t):
         ch = self._reduce
         if (self.active and ch is not None and t.dtype == torch.float64 and t.device == self.device
-                and t.is_contiguous() and 2 * t.numel() <= ch.slot_words):
+                and t.is_contiguous() and t.numel() % 2 == 0 and 2 * t.numel() <= ch.slot_words):
             ch.reduce_f64(t, self._hip._stream(self.device))
             self.ipc_calls += 1
             return
