@@ -47,6 +47,13 @@ VARIANTS = {
     "abl_w1adam": ["-DFEDMX_ABLATE=2"],           # no W1 Adam                0.912 ms (-17%)
     "abl_small": ["-DFEDMX_ABLATE=4"],            # no small-tile Adam        1.063 ms (-3%)
     "abl_adam": ["-DFEDMX_ABLATE=8"],             # no Adam at all            0.708 ms (-35%)
+    # r2 session 4: compiler scheduling knobs on the whole library, train launch
+    # (base 945.6 / 945.5 us on the same box; none kept)
+    "s_ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],                  # 1001.9 / 1000.5
+    "s_trk": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],                   # 970.6 / 1007.4
+    "s_norp": ["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule=1"],  # 957.4 / 961.0
+    "s_bias0": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],                # 947.1 / 945.3
+    "s_cyc": ["-mllvm", "-misched-cyclicpath=1"],                           # 946.7 / 945.9
     # fused verification kernel, timing-only (r2, base 24.6 us; scripts/r2_verify_ablate.sh)
     "vabl1": ["-DFEDMX_VERIFY_ABLATE=1"],         # no forward                13.4 us
     "vabl2": ["-DFEDMX_VERIFY_ABLATE=2"],         # no drift                  18.9 us
