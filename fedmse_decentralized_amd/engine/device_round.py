@@ -61,7 +61,7 @@ def fast_path_supported(fed) -> Optional[str]:
         (cfg.aggregation_mode in ("decentralized", "centralized"), f"aggregation mode {cfg.aggregation_mode}"),
         (cfg.protocol_variant == "code", "protocol variant is not 'code'"),
         (fed.update_type in ("avg", "fedprox", "mse_avg"), f"update type {fed.update_type}"),
-        (cfg.metric == "AUC", "metric is not AUC"),
+        (cfg.metric in ("AUC", "classification", "time"), f"metric {cfg.metric}"),
         # dropped clients leave at least one selection per round (k >= 1: the
         # election kernel needs a voter); larger drop sets take the host path
         (len({c for c in cfg.dropped_clients if 0 <= c < fed.N}) < max(1, int(cfg.num_participants * fed.N)),
@@ -209,6 +209,30 @@ class DeviceRound:
         self.host_agg_counts = [0] * N
 
     # ------------------------------------------------------------------------------
+    def _host_metrics(self, rec: dict) -> np.ndarray:
+        """The evaluator's non-AUC metrics (`src/Evaluator/evaluator.py:64-108`,
+        eval.evaluator.evaluate_clients) from this round's device evaluation:
+        ``classification`` = F1 at score threshold 0.5 of the round's anomaly
+        scores (the AUC plan's scores: CEN distances, or per-row MSE for the
+        AE); ``time`` = seconds of the evaluation launches (side-stream events).
+        Every rank fills its hosted clients; one host all-reduce."""
+        fed, eng, N = self.fed, self.fed.engine, self.N
+        vec = np.zeros(N, dtype=np.float64)
+        if fed.local:
+            if fed.cfg.metric == "time":
+                e0, e1 = rec["eval_timing"]
+                vec[self.start:self.start + self.n_local] = e0.elapsed_time(e1) / 1e3
+            else:
+                from ..eval.metrics import classification_metrics
+
+                p = eng._plan(fed.model_type, rec["eval_params"])
+                D = fed.dims.d_in
+                st = eng.store
+                for i, sc in enumerate(p["scores"]):
+                    s = sc / D if fed.model_type == "autoencoder" else sc
+                    vec[self.start + i] = classification_metrics(st.labels(i), s.detach().cpu().numpy())[0]
+        return np.asarray(fed.comm.all_reduce_sum(vec), dtype=np.float64)
+
     def snapshot(self) -> dict:
         """The device-resident protocol state a resumed federation needs
         (aggregation caps, every hosted receiver's verifier history and
@@ -420,7 +444,14 @@ class DeviceRound:
                 _hip.copy2_f64(self.snap_buf.dev_ptr + si * st.best.numel() * 4, best_stage.data_ptr(), nd,
                                0, 0, 0, dev)
                 rec["snap_slot"] = si
+            if cfg.metric == "time":
+                t_ev0 = torch.cuda.Event(enable_timing=True)
+                t_ev0.record(self.side)
             eng.evaluate_launch(fed.model_type, params=eval_params)
+            if cfg.metric == "time":
+                t_ev1 = torch.cuda.Event(enable_timing=True)
+                t_ev1.record(self.side)
+                rec["eval_timing"] = (t_ev0, t_ev1)
             rec["eval_params"] = eval_params   # --save-latents: the plan whose latent buffers hold this round's
             aucs_ptr = eng._plan(fed.model_type, eval_params)["aucs_buf"].dev_ptr
             if not comm.collective:
@@ -473,7 +504,9 @@ class DeviceRound:
         slot = rec["slot"]
         metrics = np.array(slot[:N], dtype=np.float64)
         rej = np.array(slot[N:2 * N], dtype=np.float64)
-        if bool(np.any(metrics == -1.0)):
+        if cfg.metric != "AUC":
+            metrics = self._host_metrics(rec)
+        elif bool(np.any(metrics == -1.0)):
             raise RuntimeError("device AUC reported a class too large for the LDS sort; disable the device "
                                "protocol (--device-protocol false) for this dataset")
         handle = rec.get("handle")
@@ -538,6 +571,6 @@ class DeviceRound:
             stop = fed.early.update(float(np.min(metrics)))
         rec.update(aggregator=aggregator, metrics=metrics, verification=verification, epochs_run=epochs_local,
                    stop=stop, done=True)
-        for key in ("handle", "snap_slot", "slot", "report", "_keep", "event", "eval_params"):
+        for key in ("handle", "snap_slot", "slot", "report", "_keep", "event", "eval_params", "eval_timing"):
             rec.pop(key, None)
         self.all_rounds.pop(rnd, None)

@@ -329,3 +329,30 @@ def test_device_round_protocol_variants_match_host_path(tmp_path, election, mode
     assert fa.agg_counts == fb.agg_counts
     if mode == "centralized":
         assert all(v == [] for v in a["ver"])
+
+
+@pytest.mark.parametrize("model_type", ["hybrid", "autoencoder"])
+def test_device_round_classification_metric_matches_host_path(tmp_path, model_type):
+    """--metric classification (F1 at threshold 0.5, the reference
+    Evaluator's alternative metric) on the device protocol: the same per-client
+    F1 as the host path's evaluator; --metric time reports positive seconds."""
+    from fedmse_decentralized_amd import federation
+    from fedmse_decentralized_amd.federation import Federation
+
+    _shrink()
+
+    def go(out, **kw):
+        federation._PREP_CACHE.clear()
+        fed = Federation(_cfg(out, save_checkpoints=False, **kw), model_type, "avg", 0).setup()
+        rs = [fed.run_round() for _ in range(3)]
+        fed.finish()
+        return fed, [r.metrics.tolist() for r in rs]
+
+    fa, a = go(str(tmp_path / "dev"), metric="classification")
+    fb, b = go(str(tmp_path / "host"), metric="classification", device_protocol=False)
+    assert fa._fast is not None and fb._fast is None
+    assert a == b
+    assert all(0.0 <= v <= 1.0 for m in a for v in m)
+    ft, t = go(str(tmp_path / "time"), metric="time")
+    assert ft._fast is not None
+    assert all(v > 0 for m in t for v in m)
