@@ -50,6 +50,16 @@ from ..ops import _hip
 log = logging.getLogger("fedmx")
 
 
+def _thesis_fused_ok(fed) -> bool:
+    """The thesis rule runs in the fused verification kernel only (it forwards
+    each receiver's rows through the aggregate and its own model in LDS)."""
+    if fed.cfg.verification_method == "dev":
+        rows = int(fed.dev_set.shape[0])
+    else:
+        rows = max((int(fed.valid_all[c].shape[0]) for c in fed.local), default=0)
+    return rows <= _hip.VERIFY_MAX_ROWS
+
+
 def fast_path_supported(fed) -> Optional[str]:
     """None when the device round can run this federation, else the reason it cannot."""
     cfg = fed.cfg
@@ -59,7 +69,8 @@ def fast_path_supported(fed) -> Optional[str]:
         (cfg.compat == "fixed", "compat mode is not 'fixed'"),
         (cfg.election in ("first_voter", "majority"), f"election {cfg.election}"),
         (cfg.aggregation_mode in ("decentralized", "centralized"), f"aggregation mode {cfg.aggregation_mode}"),
-        (cfg.protocol_variant == "code", "protocol variant is not 'code'"),
+        (cfg.protocol_variant == "code" or _thesis_fused_ok(fed),
+         "thesis variant with verification rows beyond the fused kernel's LDS buffer"),
         (fed.update_type in ("avg", "fedprox", "mse_avg"), f"update type {fed.update_type}"),
         (cfg.metric in ("AUC", "classification", "time"), f"metric {cfg.metric}"),
         # dropped clients leave at least one selection per round (k >= 1: the
@@ -202,7 +213,8 @@ class DeviceRound:
         self.n_train = {c: fed.clients[c].train.shape[0] for c in range(N)}
         # protocol variants the kernels implement: majority election (every
         # selected client votes) and the centralised push (no verification)
-        self.elect_mode = 1 if cfg.election == "majority" else 0
+        self.thesis = cfg.protocol_variant == "thesis"
+        self.elect_mode = (1 if cfg.election == "majority" else 0) | (6 if self.thesis else 0)
         self.centralized = cfg.aggregation_mode == "centralized"
         self.pending: deque = deque()
         self.all_rounds: Dict[int, dict] = {}
@@ -383,7 +395,10 @@ class DeviceRound:
             a = _hip.ElectArgs(sel=sel_ptr, vec=vec_ptr, noise=noise_ptr,
                                agg_counts=self.agg_counts.data_ptr(), weights=self.weights.data_ptr(),
                                state=self.state.data_ptr(), report=rep_ptr, k=k, cap=cfg.max_aggregation,
-                               rule=self.rule, mode=self.elect_mode, rec=rec_ptr, hw=hw_ptr)
+                               rule=self.rule, mode=self.elect_mode, rec=rec_ptr, hw=hw_ptr,
+                               vote_cap=float(cfg.thesis_vote_mse_cap),
+                               # thesis fallback: one uniform per round, drawn whatever the outcome
+                               fallback_u=fed.fallback_rng.random() if self.thesis else 0.0)
             w = _hip.WsumArgs(base=base.data_ptr(), rows=rows_ptr, weights=self.weights.data_ptr(),
                               state=self.state.data_ptr(), out=self.agg.data_ptr(), k=k, P=P_PAD)
             _hip.elect_wsum(a, w, dev)
@@ -408,9 +423,10 @@ class DeviceRound:
                                 seg=eng._seg.data_ptr(), agg_counts=self.agg_counts.data_ptr(),
                                 has_hist=self.has_hist.data_ptr(), hist_perf=self.hist_perf.data_ptr(),
                                 rejected=self.rejected.data_ptr(), rej_out=side_rep.data_ptr() + 8 * N,
-                                thr=float(cfg.verification_threshold), pthr=float(cfg.performance_threshold),
+                                thr=float(cfg.thesis_loss_ratio if self.thesis else cfg.verification_threshold),
+                                pthr=float(cfg.performance_threshold),
                                 start=self.start, n_local=self.n_local, P=P_PAD, d_in=fed.dims.d_in,
-                                mode=1 if self.centralized else 0, pad=0)
+                                mode=1 if self.centralized else (2 if self.thesis else 0), pad=0)
             if self.fused_verify:
                 # verification forward, decisions, adoption and the evaluation /
                 # artefact snapshots in one launch (bit-identical to the

@@ -43,7 +43,7 @@ from .parallel.comm import Comm, LoopbackComm
 from .parallel.sharding import ShardMap
 from .protocol.aggregation import make_plan
 from .protocol.early_stop import GlobalEarlyStop
-from .protocol.election import elect_aggregator, elect_majority, select_clients
+from .protocol.election import OneDraw, elect_aggregator, elect_majority, select_clients
 from .protocol.verification import ThesisVerifier, Verifier, VerifierState
 from .utils.rng_replay import HostNoise, TorchRngReplay
 from .utils.telemetry import Telemetry
@@ -375,8 +375,9 @@ class Federation:
                 # device protocol draws the same table)
                 k = len(selected)
                 noise = _TableNoise([float(u) for u in self.noise.rand_n(k * (k - 1))])
+            fb = OneDraw(self.fallback_rng.random()) if self.fallback_rng is not None else None
             el = elect(selected, base_scores, self.agg_counts, cfg.max_aggregation, noise,
-                       log_enabled=info, vote_mse_cap=cap, fallback_rng=self.fallback_rng)
+                       log_enabled=info, vote_mse_cap=cap, fallback_rng=fb)
             aggregator = el.aggregator
 
         verification_results: List[Dict] = []

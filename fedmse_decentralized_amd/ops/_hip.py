@@ -85,7 +85,7 @@ _vp, _i32 = ctypes.c_void_p, ctypes.c_int32
 class ElectArgs(ctypes.Structure):
     _fields_ = [("sel", _vp), ("vec", _vp), ("noise", _vp), ("agg_counts", _vp), ("weights", _vp), ("state", _vp),
                 ("report", _vp), ("k", _i32), ("cap", _i32), ("rule", _i32), ("mode", _i32), ("rec", _vp),
-                ("hw", _vp)]
+                ("hw", _vp), ("vote_cap", ctypes.c_double), ("fallback_u", ctypes.c_double)]
 
 
 class WsumArgs(ctypes.Structure):

@@ -39,14 +39,20 @@ struct ElectArgs {
   int32_t* report;         // [2] out (mapped host memory): aggregator, voter
   int32_t k, cap, rule;    // rule 0: mean (avg / fedprox), 1: 1/MSE (mse_avg),
                            // 2: host-computed weights hw (sample-weighted FedAvg)
-  int32_t mode;            // 0: first voter decides (client_trainer.py:249-285 + main.py:284-288);
-                           // 1: majority of every selected voter's ballot (legacy
-                           //    GlobalAggregator.select_aggregator; ties: selection order)
+  int32_t mode;            // bit 0 clear: first voter decides (client_trainer.py:249-285 +
+                           //   main.py:284-288); set: majority of every selected voter's ballot
+                           //   (legacy GlobalAggregator.select_aggregator; ties: selection order);
+                           // bit 1: thesis vote cap (candidates scored above vote_cap, or NaN,
+                           //   are never voted for, Thesis p.20 Alg. 4.2);
+                           // bit 2: thesis random fallback when nobody was voted for (Thesis
+                           //   p.25 §4.3.4): eligible[floor(fallback_u * n_eligible)]
   const int32_t* rec;      // [k] record index (4-double units into vec) of each selection, or
                            // null: the client id (multi-rank: records read in place from the exchange buffer)
   const float* hw;         // rule 2: [k] weights (they depend on the selection only)
+  double vote_cap;         // mode bit 1
+  double fallback_u;       // mode bit 2: this round's uniform draw (host, every round)
 };
-static_assert(sizeof(ElectArgs) == 88, "ElectArgs layout is shared with Python");
+static_assert(sizeof(ElectArgs) == 104, "ElectArgs layout is shared with Python");
 
 struct WsumArgs {
   const float* base;       // row-major [*, P]
@@ -95,7 +101,7 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
       }
       int agg = -1, voter = -1;
       int my_votes = 0;   // majority: ballots naming this lane's client
-      for (int vi = 0; vi < k && (agg < 0 || E.mode == 1); ++vi) {
+      for (int vi = 0; vi < k && (agg < 0 || (E.mode & 1)); ++vi) {
         const int v = __shfl(c, vi, 64);
         // candidate lane ci != vi draws noise entry j = ci - (ci > vi)
         bool cand = lane < k && lane != vi && cnt < E.cap;
@@ -104,6 +110,7 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
           const double f = 1.0 + (E.noise[(size_t)vi * (k - 1) + lane - (lane > vi ? 1 : 0)] - 0.5) * 0.0002;
           sc = vs * f;
         }
+        if (E.mode & 2) cand = cand && (sc <= E.vote_cap);
         // the serial scan of the reference loop over the candidates' lanes
         // (uniform across the wave; NaN scores behave exactly as there)
         int best = -1;
@@ -122,7 +129,7 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
           if (lane == best) ++my_votes;
         }
       }
-      if (E.mode == 1) {
+      if (E.mode & 1) {
         // most ballots wins, ties to the earliest in selection order
         int top = -1, top_votes = 0;
         for (int ci = 0; ci < k; ++ci) {
@@ -134,6 +141,26 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
         }
         agg = top >= 0 ? __shfl(c, top, 64) : -1;
         voter = -1;
+      }
+      if (agg < 0 && (E.mode & 4)) {
+        // random eligible aggregator: the idx-th eligible lane in selection order
+        const unsigned long long m = __ballot(lane < k && cnt < E.cap);
+        const int n_e = __popcll(m);
+        if (n_e > 0) {
+          int idx = (int)(E.fallback_u * (double)n_e);
+          if (idx > n_e - 1) idx = n_e - 1;
+          int pick = 0, seen = 0;
+          for (int ci = 0; ci < k; ++ci)
+            if ((m >> ci) & 1ull) {
+              if (seen == idx) {
+                pick = ci;
+                break;
+              }
+              ++seen;
+            }
+          agg = __shfl(c, pick, 64);
+          voter = -1;
+        }
       }
       if (lane == 0) s_agg = agg;
       if (agg >= 0) {
@@ -162,9 +189,9 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
   } else if (tid == 0) {
     int agg = -1, voter = -1;
     int* s_votes = reinterpret_cast<int*>(s_w);   // majority tally (s_w is written after it)
-    if (E.mode == 1)
+    if (E.mode & 1)
       for (int j = 0; j < E.k; ++j) s_votes[j] = 0;
-    for (int vi = 0; vi < E.k && (agg < 0 || E.mode == 1); ++vi) {
+    for (int vi = 0; vi < E.k && (agg < 0 || (E.mode & 1)); ++vi) {
       const int v = E.sel[vi];
       const double* u = E.noise + (size_t)vi * (E.k - 1);
       int best = -1, best_ci = -1, j = 0;
@@ -174,7 +201,7 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
         if (c == v) continue;
         const double f = 1.0 + (u[j++] - 0.5) * 0.0002;
         const double sc = E.vec[(size_t)(E.rec != nullptr ? E.rec[ci] : c) * 4] * f;
-        if (E.agg_counts[c] < E.cap && (best < 0 || sc < best_s)) {
+        if (E.agg_counts[c] < E.cap && (!(E.mode & 2) || sc <= E.vote_cap) && (best < 0 || sc < best_s)) {
           best = c;
           best_ci = ci;
           best_s = sc;
@@ -183,10 +210,10 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
       if (best >= 0) {
         agg = best;
         voter = v;
-        if (E.mode == 1) ++s_votes[best_ci];
+        if (E.mode & 1) ++s_votes[best_ci];
       }
     }
-    if (E.mode == 1) {
+    if (E.mode & 1) {
       int top = -1, top_votes = 0;
       for (int ci = 0; ci < E.k; ++ci)
         if (s_votes[ci] > top_votes) {
@@ -195,6 +222,23 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
         }
       agg = top >= 0 ? E.sel[top] : -1;
       voter = -1;
+    }
+    if (agg < 0 && (E.mode & 4)) {
+      int n_e = 0;
+      for (int j = 0; j < E.k; ++j) n_e += E.agg_counts[E.sel[j]] < E.cap ? 1 : 0;
+      if (n_e > 0) {
+        int idx = (int)(E.fallback_u * (double)n_e);
+        if (idx > n_e - 1) idx = n_e - 1;
+        for (int j = 0, seen = 0; j < E.k; ++j)
+          if (E.agg_counts[E.sel[j]] < E.cap) {
+            if (seen == idx) {
+              agg = E.sel[j];
+              break;
+            }
+            ++seen;
+          }
+        voter = -1;
+      }
     }
     s_agg = agg;
     if (agg >= 0) {
@@ -286,7 +330,10 @@ struct DecideArgs {
   int32_t start, n_local, P, d_in;
   int32_t mode;            // 0: receivers verify (ModelVerifier); 1: centralised push (legacy
                            //    GlobalAggregator.update): every hosted client, the aggregator
-                           //    included, loads the aggregate and re-anchors FedProx, no verification
+                           //    included, loads the aggregate and re-anchors FedProx, no verification;
+                           // 2: thesis rule (Thesis p.20-22 Alg. 4.3): accept iff the aggregate's
+                           //    MSE on the receiver's data is finite and <= (1 + thr) x the MSE of
+                           //    the receiver's own current model there (fused kernel only)
   int32_t pad;
 };
 static_assert(sizeof(DecideArgs) == 152, "DecideArgs layout is shared with Python");
@@ -473,8 +520,7 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     }
     __syncthreads();
     // ---- MSE (score_reduce / decide_adopt order)
-    double mse;
-    {
+    auto mse_of_rows = [&]() -> double {
       const int n = d.nrows;
       double sv = 0.0;
       if (tid < 256) {
@@ -485,7 +531,18 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
       if (lane == 0 && wv < 4) s_d[wv] = sv;
       __syncthreads();
       const double tot = s_d[0] + s_d[1] + s_d[2] + s_d[3];
-      mse = n > 0 ? tot / ((double)n * A.d_in) : __builtin_nan("");
+      __syncthreads();   // s_d / s_sse reusable
+      return n > 0 ? tot / ((double)n * A.d_in) : __builtin_nan("");
+    };
+    const double mse = mse_of_rows();
+    double old_mse = 0.0;
+    if (A.mode == 2) {
+      // thesis rule: the receiver's own current model on the same rows
+      stage_params<CP>(A.params + off, sW1, sW2, sW3, sW4);
+      __syncthreads();
+      fwd_rows_block<CP>(d, sW1, sW2, sW3, sW4, wv, 8, s_sse);
+      __syncthreads();
+      old_mse = mse_of_rows();
     }
     // ---- drift of the receiver's history vs the aggregate (param_drift order:
     // virtual threads vt = tid and tid + 512 of a 1024-thread block, each
@@ -493,7 +550,7 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     // thread's loads are issued before the first add: one memory round trip
     // instead of one per 4 elements (6 dependent rounds, ~5 us of the kernel).
     float drift = 0.f;
-    if (had_hist && !(FEDMX_VERIFY_ABLATE & 2)) {
+    if (had_hist && A.mode == 0 && !(FEDMX_VERIFY_ABLATE & 2)) {
       const float* h = A.hist + off;
       constexpr int NJ = (P_PAD + 1023) / 1024;
       int sg[2][NJ];
@@ -539,7 +596,10 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     if (tid == 0) {
       const double perf = 1.0 / (1.0 + mse);
       int okk;
-      if (!had_hist) {
+      if (A.mode == 2) {
+        okk = __builtin_isfinite(mse) && mse <= old_mse * (1.0 + A.thr);
+        A.has_hist[cl] = 1;
+      } else if (!had_hist) {
         okk = 1;  // the first received model is accepted unconditionally
         A.has_hist[cl] = 1;
       } else {

@@ -74,8 +74,27 @@ def _ballot(voter: int, selected: Sequence[int], base_scores: Dict[int, float], 
 
 
 def _fallback(selected, agg_counts, max_aggregation, rng) -> Optional[int]:
+    """Uniform choice among the eligible selected clients from ONE uniform
+    draw ``u = rng.random()``: ``eligible[floor(u * n)]`` (the device
+    protocol's election kernel applies the same formula to the same draw)."""
     eligible = [c for c in selected if agg_counts[c] < max_aggregation]
-    return rng.choice(eligible) if eligible else None
+    if not eligible:
+        return None
+    n = len(eligible)
+    return eligible[min(int(rng.random() * n), n - 1)]
+
+
+class OneDraw:
+    """A pre-drawn uniform for :func:`_fallback`: the federation draws one
+    value per round whether or not the fallback is needed, so the random
+    stream does not depend on the election's outcome (and the device
+    protocol, which learns the outcome only on the GPU, consumes it alike)."""
+
+    def __init__(self, u: float):
+        self.u = float(u)
+
+    def random(self) -> float:
+        return self.u
 
 
 def elect_aggregator(selected: Sequence[int], base_scores: Dict[int, float], agg_counts: Sequence[int],

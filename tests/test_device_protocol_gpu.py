@@ -356,3 +356,23 @@ def test_device_round_classification_metric_matches_host_path(tmp_path, model_ty
     ft, t = go(str(tmp_path / "time"), metric="time")
     assert ft._fast is not None
     assert all(v > 0 for m in t for v in m)
+
+
+@pytest.mark.parametrize("election,vote_cap", [("first_voter", 3.0), ("first_voter", 1e-9), ("majority", 1e-9)])
+def test_device_round_thesis_variant_matches_host_path(tmp_path, election, vote_cap):
+    """The thesis protocol (Thesis p.20-26: vote-MSE cap, random eligible
+    aggregator when nobody is voted for, loss-ratio acceptance against the
+    receiver's own model) on the device protocol matches the host path; a
+    tiny cap forces the random fallback every round."""
+    _shrink()
+    kw = dict(save_checkpoints=False, protocol_variant="thesis", election=election, thesis_vote_mse_cap=vote_cap)
+    fa, a = _run(_cfg(str(tmp_path / "dev"), **kw), "mse_avg", 5)
+    fb, b = _run(_cfg(str(tmp_path / "host"), device_protocol=False, **kw), "mse_avg", 5)
+    assert fa._fast is not None and fb._fast is None
+    assert a["sel"] == b["sel"] and a["agg"] == b["agg"] and a["ver"] == b["ver"]
+    assert all(x is not None for x in a["agg"])
+    for x, y in zip(a["metrics"], b["metrics"]):
+        np.testing.assert_array_equal(np.array(x), np.array(y))
+    assert torch.equal(fa.engine.store.params, fb.engine.store.params)
+    assert torch.equal(fa.engine.store.anchor, fb.engine.store.anchor)
+    assert fa.agg_counts == fb.agg_counts
