@@ -607,6 +607,7 @@ class Federation:
                                 int(s.history_round), int(s.rejected_updates)] for c, s in self.vstate.items()},
             "versions": {int(v): self.versions[v].cpu() for v in vers},
             "py_rng": _py_state_to_list(self.py_rng.getstate()),
+            "fallback_rng": _py_state_to_list(self.fallback_rng.getstate()) if self.fallback_rng is not None else [],
             "noise_state": self.noise.state.clone() if isinstance(self.noise, TorchRngReplay) else torch.zeros(0),
             "early": [float(self.early.best), int(self.early.worse)],
             "last_metrics": torch.from_numpy(self.last_metrics) if self.last_metrics is not None else torch.zeros(0),
@@ -629,6 +630,8 @@ class Federation:
             self.vstate[int(c)] = VerifierState(None if hv < 0 else hv, hp, hr, rej)
         self.versions = {int(v): t.to(st.params.device) for v, t in s["versions"].items()}
         self.py_rng.setstate(_py_state_from_list(s["py_rng"]))
+        if self.fallback_rng is not None and s.get("fallback_rng"):
+            self.fallback_rng.setstate(_py_state_from_list(s["fallback_rng"]))
         if isinstance(self.noise, TorchRngReplay) and s["noise_state"].numel():
             self.noise.state = s["noise_state"].clone()
         self.early.best, self.early.worse = float(s["early"][0]), int(s["early"][1])

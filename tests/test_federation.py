@@ -86,22 +86,27 @@ def test_model_cpt_bytes_match_reference_writer(tmp_path):
     assert list(a) == list(b) and all(torch.equal(a[k], b[k]) for k in a)
 
 
-@pytest.mark.parametrize("compat", ["reference", "fixed"])
-def test_resume_reproduces_trajectory(tmp_path, compat):
+@pytest.mark.parametrize("compat,variant", [("reference", "code"), ("fixed", "code"), ("fixed", "thesis")])
+def test_resume_reproduces_trajectory(tmp_path, compat, variant):
     """Resume from a per-round snapshot: both the reference-RNG replay and the
     fixed mode's seeded tie-break noise stream continue where they stopped."""
-    cfg = _cfg(tmp_path, global_early_stop=False, num_rounds=4, save_checkpoints=False, compat=compat)
+    cfg = _cfg(tmp_path, global_early_stop=False, num_rounds=4, save_checkpoints=False, compat=compat,
+               protocol_variant=variant)
     a = Federation(cfg, "hybrid", "avg", 0).setup()
     for _ in range(2):
         a.run_round()
     snap = a.save_snapshot(str(tmp_path / "snap.pt"))
     noise_at_snap = a.noise.get_state() if compat == "fixed" else None
+    fb_at_snap = a.fallback_rng.getstate() if variant == "thesis" else None
     ra = [a.run_round().metrics for _ in range(2)]
-    cfg2 = _cfg(tmp_path, global_early_stop=False, num_rounds=4, save_checkpoints=False, resume=snap, compat=compat)
+    cfg2 = _cfg(tmp_path, global_early_stop=False, num_rounds=4, save_checkpoints=False, resume=snap, compat=compat,
+                protocol_variant=variant)
     b = Federation(cfg2, "hybrid", "avg", 0).setup()
     assert b.round_idx == 2
     if compat == "fixed":
         assert b.noise.get_state() == noise_at_snap
+    if variant == "thesis":
+        assert b.fallback_rng.getstate() == fb_at_snap
     rb = [b.run_round().metrics for _ in range(2)]
     for x, y in zip(ra, rb):
         np.testing.assert_array_equal(x, y)
