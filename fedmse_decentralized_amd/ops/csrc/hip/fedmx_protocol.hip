@@ -483,8 +483,19 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
   __shared__ float part[8][16];
   const int a = A.state[0];
   if (a >= 0 && blockIdx.x == 0 && threadIdx.x == 0) A.agg_counts[a] += 1;
+  if ((int)blockIdx.x >= A.n_local) {
+    // workgroups n_local..2n_local-1: the artefact snapshot best -> best_stage
+    // of client blockIdx.x - n_local (independent of every decision, so it
+    // runs beside the verification instead of in its adoption pass)
+    const int cl2 = blockIdx.x - A.n_local;
+    if (cl2 >= A.n_local || (FEDMX_VERIFY_ABLATE & 4)) return;
+    const size_t o2 = (size_t)cl2 * A.P;
+    const f32x4* b = reinterpret_cast<const f32x4*>(V.best + o2);
+    f32x4* bs = reinterpret_cast<f32x4*>(V.best_stage + o2);
+    for (int i = threadIdx.x; i < A.P / 4; i += blockDim.x) bs[i] = b[i];
+    return;
+  }
   const int cl = blockIdx.x;
-  if (cl >= A.n_local) return;
   const int c = A.start + cl;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
@@ -493,8 +504,6 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
   const f32x4* src = reinterpret_cast<const f32x4*>(A.agg);
   f32x4* prm = reinterpret_cast<f32x4*>(A.params + off);
   f32x4* evp = reinterpret_cast<f32x4*>(V.eval_params + off);
-  f32x4* bst = reinterpret_cast<f32x4*>(V.best_stage + off);
-  const f32x4* bsrc = reinterpret_cast<const f32x4*>(V.best + off);
   bool ok = false, load = false;
   if (a >= 0 && A.mode == 1) {
     load = ok = true;   // centralised push: every hosted client loads and re-anchors
@@ -620,14 +629,13 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
   if (FEDMX_VERIFY_ABLATE & 4) return;
   const bool receiver = a >= 0 && c != a && A.mode == 0;
   constexpr int UA = (P_PAD / 4 + 511) / 512;   // every element of the row in one pass of loads
-  f32x4 v[UA], pv[UA], bv[UA];
+  f32x4 v[UA], pv[UA];
 #pragma unroll
   for (int u = 0; u < UA; ++u) {
     const int i = tid + 512 * u;
     if (i < n4) {
       v[u] = src[i];
       pv[u] = load ? v[u] : prm[i];
-      bv[u] = bsrc[i];
     }
   }
 #pragma unroll
@@ -640,7 +648,6 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
       }
       if (receiver) reinterpret_cast<f32x4*>(A.hist + off)[i] = v[u];
       evp[i] = pv[u];
-      bst[i] = bv[u];
     }
   }
 }
@@ -721,7 +728,8 @@ int fedmx_elect_wsum(const void* eargs, const void* wargs, hipStream_t stream) {
 int fedmx_verify_decide(const void* args, hipStream_t stream) {
   const fedmx::VerifyArgs& V = *reinterpret_cast<const fedmx::VerifyArgs*>(args);
   if (V.D.P % 4 != 0 || V.D.P != fedmx::P_PAD) return -1;
-  const dim3 grid(V.D.n_local > 0 ? V.D.n_local : 1);
+  // n_local verification workgroups + n_local snapshot-copy workgroups
+  const dim3 grid(V.D.n_local > 0 ? 2 * V.D.n_local : 1);
   // compact forward order for the reference shapes (fedmx_forward_common.h)
   if (V.D.d_in <= 115 && V.hidden <= 27 && V.latent <= 7)
     hipLaunchKernelGGL(fedmx::verify_decide_kernel<true>, grid, dim3(512), 0, stream, V);
