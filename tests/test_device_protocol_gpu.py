@@ -376,3 +376,43 @@ def test_device_round_thesis_variant_matches_host_path(tmp_path, election, vote_
     assert torch.equal(fa.engine.store.params, fb.engine.store.params)
     assert torch.equal(fa.engine.store.anchor, fb.engine.store.anchor)
     assert fa.agg_counts == fb.agg_counts
+
+
+def _worker_kw(rank, world, port, out, kw):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), FEDMX_DEVICE_INDEX="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    _shrink()
+    from fedmse_decentralized_amd.parallel.launch import init_comm, shutdown
+
+    comm = init_comm(backend="gloo", device="cuda")
+    fed, res = _run(_cfg(os.path.join(out, f"r{rank}"), save_checkpoints=False, debug_replica_check=True, **kw),
+                    "mse_avg", 4, comm=comm)
+    res["fast"] = fed._fast is not None
+    res["params"] = fed.engine.store.params.double().sum(1).tolist()
+    res["local"] = fed.local
+    with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
+        json.dump(res, f)
+    shutdown(comm)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("kw", [dict(protocol_variant="thesis", election="majority"),
+                                dict(metric="classification", fedavg_sample_weighted=True),
+                                dict(aggregation_mode="centralized", dropped_clients=[2])])
+def test_device_round_variants_multi_rank_one_gpu(tmp_path, kw):
+    """Protocol variants on the device path with two gloo ranks sharing one
+    GPU: every rank reaches the single-process run's decisions, metrics and
+    parameters (replicated state checked every round)."""
+    out = str(tmp_path)
+    mp.start_processes(_worker_kw, args=(2, _port(), out, kw), nprocs=2, join=True, start_method="spawn")
+    _shrink()
+    fed, ref = _run(_cfg(os.path.join(out, "single"), save_checkpoints=False, **kw), "mse_avg", 4)
+    ref_params = fed.engine.store.params.double().sum(1).tolist()
+    for r in range(2):
+        d = json.load(open(os.path.join(out, f"rank{r}.json")))
+        assert d["fast"]
+        assert d["agg"] == ref["agg"] and d["sel"] == ref["sel"] and d["ver"] == ref["ver"]
+        for x, y in zip(d["metrics"], ref["metrics"]):
+            np.testing.assert_array_equal(np.array(x), np.array(y))
+        loc = d["local"]
+        assert d["params"] == ref_params[loc[0]:loc[-1] + 1]
