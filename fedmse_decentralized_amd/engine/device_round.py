@@ -50,6 +50,11 @@ from ..ops import _hip
 log = logging.getLogger("fedmx")
 
 
+# A/B timing only: pack the multi-rank send buffer with its own copy_rows
+# launch instead of inside the score-reduction launch
+_PACK_SEPARATE = os.environ.get("FEDMX_PACK_SEPARATE", "0") == "1"
+
+
 def _thesis_fused_ok(fed) -> bool:
     """The thesis rule runs in the fused verification kernel only (it forwards
     each receiver's rows through the aggregate and its own model in LDS)."""
@@ -327,7 +332,11 @@ class DeviceRound:
                     outs += [p + 16 for p in recp]
                     batch += [0] * len(local_rows)
                 sse, _ = _hip.forward_rows(st.params, items, fed.dims, True, False)
-                _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs)
+                # multi-rank: the exchange's pack (row 1 + j of the send buffer =
+                # the j-th local selection's parameters) rides the same launch
+                copies = [(st.params[self._loc(c)].data_ptr(), self.xsend[1 + j].data_ptr(), P_PAD)
+                          for j, c in enumerate(local_sel)] if comm.collective and not _PACK_SEPARATE else ()
+                _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs, copies)
         with tel.phase("comm"):
             if not comm.collective:
                 base = st.params
@@ -355,10 +364,12 @@ class DeviceRound:
                 send = self.xsend[:slots + 1]
                 allg = self.xallg[:comm.world_size * (slots + 1)]
                 if mine:
-                    # (the vote records are already in row 0: score_reduce wrote them there)
-                    (loc_ptr,) = self.rt.desc.put(np.asarray([self._loc(c) for c in mine], dtype=np.int32))
-                    _hip.copy_rows(send[1].data_ptr(), P_PAD, 0, st.params.data_ptr(), P_PAD, loc_ptr, len(mine),
-                                   P_PAD, dev)
+                    # (the vote records are already in row 0 and the models in
+                    # rows 1.. : the score-reduction launch wrote / copied them)
+                    if _PACK_SEPARATE:   # A/B: the pack as a launch of its own
+                        (loc_ptr,) = self.rt.desc.put(np.asarray([self._loc(c) for c in mine], dtype=np.int32))
+                        _hip.copy_rows(send[1].data_ptr(), P_PAD, 0, st.params.data_ptr(), P_PAD, loc_ptr,
+                                       len(mine), P_PAD, dev)
                     if comm.phantom and len(mine) < slots:
                         # single-GPU projection (PhantomComm): other ranks' rows are
                         # copies of this rank's, so the spare slots must hold real models

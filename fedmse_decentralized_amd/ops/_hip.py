@@ -138,6 +138,7 @@ def lib():
                 "fedmx_cen_score": [vp, i32, vp],
                 "fedmx_auc": [vp, i32, vp],
                 "fedmx_score_reduce": [vp, i32, i32, vp],
+                "fedmx_score_reduce_copy": [vp, i32, i32, vp, i32, vp],
                 "fedmx_broadcast_rows": [vp, vp, vp, i32, vp, i32, vp],
                 "fedmx_train": [ctypes.POINTER(TrainArgs), i32, vp],
                 "fedmx_train8": [ctypes.POINTER(TrainArgs), i32, vp],
@@ -528,9 +529,15 @@ def score_reduce(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in: i
     return view.reshape(len(sse_list), 2)
 
 
-def score_reduce_to(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in: int, out_ptrs: Sequence[int]):
+COPY_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("nfloats", "<i4"), ("pad", "<i4")])
+
+
+def score_reduce_to(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in: int, out_ptrs: Sequence[int],
+                    copies: Sequence[Tuple[int, int, int]] = ()):
     """score_reduce writing each segment's (vote score, MSE) pair to the given
-    device addresses (16 bytes each) instead of the result ring."""
+    device addresses (16 bytes each) instead of the result ring.  ``copies``
+    (src, dst, nfloats): row copies that run in the same launch, beside the
+    reductions (the multi-rank exchange's pack)."""
     dev = sse_list[0].device
     rt = runtime(dev)
     desc = np.zeros(len(sse_list), dtype=SEG_DTYPE)
@@ -538,8 +545,18 @@ def score_reduce_to(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in
     desc["n"] = [int(s.shape[0]) for s in sse_list]
     desc["batch"] = list(batch)
     desc["out"] = np.asarray(out_ptrs, dtype=np.int64)
-    (dptr,) = rt.desc.put(desc)
-    _check(lib().fedmx_score_reduce(dptr, len(desc), d_in, rt.stream), "fedmx_score_reduce")
+    if not copies:
+        (dptr,) = rt.desc.put(desc)
+        _check(lib().fedmx_score_reduce(dptr, len(desc), d_in, rt.stream), "fedmx_score_reduce")
+        return
+    cd = np.zeros(len(copies), dtype=COPY_DTYPE)
+    cd["src"] = [c[0] for c in copies]
+    cd["dst"] = [c[1] for c in copies]
+    cd["nfloats"] = [c[2] for c in copies]
+    if bool(np.any(cd["nfloats"] % 4)):
+        raise ValueError("score_reduce_to: copies must move whole float4 words")
+    dptr, cptr = rt.desc.put(desc, cd)
+    _check(lib().fedmx_score_reduce_copy(dptr, len(desc), d_in, cptr, len(cd), rt.stream), "fedmx_score_reduce_copy")
 
 
 def seg_desc_device(sse_list: Sequence[torch.Tensor], batch: Sequence[int], out_ptrs: Sequence[int], dev) -> torch.Tensor:

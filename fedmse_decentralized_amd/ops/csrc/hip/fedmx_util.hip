@@ -43,8 +43,7 @@ __device__ __forceinline__ double block_sum_d(double v, double* s_w) {
 // four per thread in flight, so the latency-bound pass is a few round trips
 // instead of one per 256 rows; batched segments (the 128-row vote batches)
 // are reduced one batch after another.
-__global__ __launch_bounds__(SCORE_THREADS) void score_reduce_kernel(const SegDesc* __restrict__ descs, int d_in) {
-  const SegDesc d = descs[blockIdx.x];
+__device__ __forceinline__ void score_reduce_block(const SegDesc& d, int d_in) {
   __shared__ double s_w[SCORE_WAVES];
   const int tid = threadIdx.x;
   const int bs = d.batch > 0 ? d.batch : (d.n > 0 ? d.n : 1);
@@ -89,6 +88,35 @@ __global__ __launch_bounds__(SCORE_THREADS) void score_reduce_kernel(const SegDe
     d.out[0] = nb > 0 ? vote / nb : __builtin_inf();
     d.out[1] = d.n > 0 ? tot / ((double)d.n * d_in) : __builtin_nan("");
   }
+}
+
+__global__ __launch_bounds__(SCORE_THREADS) void score_reduce_kernel(const SegDesc* __restrict__ descs, int d_in) {
+  score_reduce_block(descs[blockIdx.x], d_in);
+}
+
+// row copies riding the same launch (the multi-rank exchange's pack of the
+// locally selected models into the send buffer: it needs the trained
+// parameters only, so it runs beside the score reduction instead of as a
+// launch of its own on the round's critical path)
+struct CopyDesc {
+  const float* src;
+  float* dst;
+  int32_t nfloats;   // multiple of 4
+  int32_t pad;
+};
+static_assert(sizeof(CopyDesc) == 24, "CopyDesc layout is shared with Python");
+
+__global__ __launch_bounds__(SCORE_THREADS) void score_reduce_copy_kernel(const SegDesc* __restrict__ descs, int n,
+                                                                          int d_in,
+                                                                          const CopyDesc* __restrict__ copies) {
+  if ((int)blockIdx.x < n) {
+    score_reduce_block(descs[blockIdx.x], d_in);
+    return;
+  }
+  const CopyDesc c = copies[blockIdx.x - n];
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(c.src);
+  f32x4* d4 = reinterpret_cast<f32x4*>(c.dst);
+  for (int i = threadIdx.x; i < c.nfloats / 4; i += SCORE_THREADS) d4[i] = s4[i];
 }
 
 __global__ __launch_bounds__(256) void broadcast_rows_kernel(float* __restrict__ dst0, float* __restrict__ dst1,
@@ -179,6 +207,14 @@ __global__ __launch_bounds__(1024) void standardize_lds_kernel(const float* __re
 }  // namespace fedmx
 
 extern "C" {
+
+int fedmx_score_reduce_copy(const void* descs, int n, int d_in, const void* copies, int ncopy, hipStream_t stream) {
+  if (n + ncopy <= 0) return 0;
+  hipLaunchKernelGGL(fedmx::score_reduce_copy_kernel, dim3(n + ncopy), dim3(fedmx::SCORE_THREADS), 0, stream,
+                     reinterpret_cast<const fedmx::SegDesc*>(descs), n, d_in,
+                     reinterpret_cast<const fedmx::CopyDesc*>(copies));
+  return (int)hipGetLastError();
+}
 
 int fedmx_score_reduce(const void* descs, int n, int d_in, hipStream_t stream) {
   if (n <= 0) return 0;
