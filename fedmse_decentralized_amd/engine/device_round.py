@@ -8,16 +8,20 @@ a host RNG whose consumption does not depend on results, so the whole round
 can be *enqueued* instead:
 
     train (fused kernel, all local selected clients)
-    (side stream, overlapping training: standardise the vote data)
     forward + score_reduce -> vec[N,4] (vote score, dev MSE)
-    [pack + ONE RCCL all-gather: the selected models + their vote records]
-    elect_wsum_kernel       aggregator, FedAvg / FedMSE weights, aggregate
-    forward(agg, every hosted client's verification data)
-    decide_adopt_kernel     MSE + drift reductions, ModelVerifier rule, adoption,
-                            history update, aggregation-cap count
-    snapshot params / best models (one fused device copy)
+                            [with collectives: records straight into the send
+                            buffer's row 0, the pack of the selected models in
+                            extra workgroups of the same launch]
+    [ONE all-gather (RCCL, or --comm ipc): the selected models + their vote records]
+    elect_wsum_kernel       aggregator (first voter / majority, thesis cap and
+                            fallback), FedAvg / FedMSE / sample weights, aggregate
+    verify_decide_kernel    fused: forward(agg, every hosted client's verification
+                            data) [+ own model: thesis], MSE + drift reductions,
+                            ModelVerifier / thesis rule (or centralised push),
+                            adoption, history, aggregation-cap count, evaluation
+                            snapshot; artefact snapshot in extra workgroups
     side stream: best models -> mapped host snapshot slot, evaluation (fwd + CEN + AUC)
-                 [one RCCL all-reduce: AUCs + rejected counts] -> mapped per-round
+                 [one all-reduce: AUCs + rejected counts] -> mapped per-round
                  report slot; record the round event
                  (overlaps the next round's training; the next round's
                  verification waits for it before reusing the buffers)
@@ -30,8 +34,11 @@ A round therefore costs its GPU time only; the host work of round r+1
 overlaps the GPU work of round r.
 
 Decisions, aggregates and metrics are identical to the host path in fixed
-mode (tested on the GPU); the host-side RNG draws one k x (k-1) noise table
-per round in both paths.
+mode (tested on the GPU, and over 60 bench-shaped rounds:
+scripts/device_vs_host_long.py); the host-side RNG draws one k x (k-1) noise
+table per round in both paths (and, in the thesis variant, one fallback
+uniform).  Resume snapshots (``snapshot`` / ``restore``), latent logging,
+fault injection and the non-AUC metrics run on this path too.
 """
 from __future__ import annotations
 
