@@ -91,6 +91,14 @@ class ExperimentConfig:
     protocol_variant: str = "code"
     thesis_loss_ratio: float = 0.1
     thesis_vote_mse_cap: float = 3.0
+    # initial client models: "per_client" builds one independently initialised
+    #   model per client (the reference, src/main.py:228-236); "shared" gives
+    #   every client a copy of client 0's initial model (one global init, as
+    #   the FedMSE paper's server does).  "auto": per_client under
+    #   compat=reference, shared under compat=fixed — averaging k independent
+    #   inits cancels the latent layer by ~sqrt(k), which large federations
+    #   never recover from (profiles/r3_collapse_diag.md).
+    init_mode: str = "auto"
     fusion_max_rows: int = 1024          # dev rows used by the fusion_avg KDE similarity
     fedavg_sample_weighted: bool = False  # FedAvg weights ∝ training-set size (reference: plain mean, Q13)
     # experiment-level parallelism: with N ranks, combination
@@ -127,6 +135,13 @@ class ExperimentConfig:
     def client_save_dir(self, run: int, model_type: str, update_type: str, device_name: str) -> str:
         return os.path.join(self.output_root, f"Checkpoint/{self.network_size}/{self.experiment_name}/{run}/ClientModel",
                             self.scen_name, model_type, update_type, device_name)
+
+    def resolved_init_mode(self) -> str:
+        if self.init_mode == "auto":
+            return "per_client" if self.compat == "reference" else "shared"
+        if self.init_mode not in ("per_client", "shared"):
+            raise ValueError(f"init_mode must be auto | per_client | shared, got {self.init_mode!r}")
+        return self.init_mode
 
     def resolved_device(self) -> str:
         if self.device == "auto":

@@ -491,12 +491,16 @@ class DeviceRound:
             if not comm.collective:
                 _hip.copy2_f64(slot_ptr, aucs_ptr, N, slot_ptr + 8 * N, side_rep.data_ptr() + 8 * N, N, dev)
             else:
-                # [AUCs | rejected counts]: one RCCL all-reduce, off the main stream
-                side_rep[:N].zero_()
+                # [AUCs | rejected counts]: one RCCL all-reduce, off the main stream.
+                # Every entry this rank does not write must be zero going in: the
+                # slot is cleared right after its sum is copied out (so when the
+                # slot comes round again, only this round's verification has
+                # written it — the hosted receivers' counts)
                 if self.n_local:
                     _hip.copy_f64(side_rep.data_ptr() + 8 * self.start, aucs_ptr, self.n_local, dev)
                 comm.all_reduce_inplace(side_rep)
                 _hip.copy_f64(slot_ptr, side_rep.data_ptr(), 2 * N, dev)
+                side_rep.zero_()
             ev = torch.cuda.Event()
             ev.record(self.side)
             side["ev"] = ev

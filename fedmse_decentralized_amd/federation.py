@@ -164,6 +164,10 @@ class Federation:
         self.shard = ShardMap(N, self.comm.world_size)
         self.local = self.shard.local_ids(self.comm.rank)
         init, rng_state = init_client_params(N, self.run * 10000, self.dims)
+        if cfg.resolved_init_mode() == "shared":
+            # one global initial model (the RNG state after all N inits is kept,
+            # so the reference's draw order downstream is unchanged)
+            init = init[:1].expand(N, -1).clone()
         self.noise = TorchRngReplay(rng_state, self.dims) if cfg.compat == "reference" else HostNoise(self.run * 10000 + 17)
         eng = self.engine
         loc = [clients[c] for c in self.local]

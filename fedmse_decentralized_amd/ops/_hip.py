@@ -282,8 +282,11 @@ def fwd_rows_per_block(total_rows: int, n_items: int) -> int:
         return -(-int(total_rows) // rpb) + n_items
 
     waves = blocks(per) / FWD_RESIDENT
-    if waves > 1 and waves - int(waves) < 0.25:
-        while blocks(per) > FWD_RESIDENT * int(waves):
+    target = FWD_RESIDENT * int(waves)
+    # every item keeps at least one block: growing the blocks can only help
+    # while the items alone fit in the target (else the loop would never end)
+    if waves > 1 and waves - int(waves) < 0.25 and n_items + 1 <= target:
+        while blocks(per) > target and per < total_rows:
             per += 64
     return int(per)
 

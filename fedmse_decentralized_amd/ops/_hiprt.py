@@ -143,6 +143,12 @@ class DeviceWriteBuffer:
         self.host_ptr = p.value
         self.dev_ptr = p.value
         self.nbytes = nbytes
+        # without a CPU mapping of the allocation (no large-BAR access) the
+        # first host store would fault: check the process's page mappings first
+        if not _cpu_mapped_rw(self.host_ptr, nbytes):
+            L.hipFree(ctypes.c_void_p(self.host_ptr))
+            self.host_ptr = None
+            raise RuntimeError("fine-grained device memory is not mapped for host access (no large BAR)")
         self.np = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.host_ptr))
         # the host's stores must reach the device copy: write a pattern, read
         # it back through the runtime (device -> host copy), else refuse
@@ -164,6 +170,32 @@ class DeviceWriteBuffer:
             self.host_ptr = None
         except Exception:
             pass
+
+
+def _cpu_mapped_rw(addr: int, nbytes: int, maps_path: str = "/proc/self/maps") -> bool:
+    """True when [addr, addr + nbytes) lies inside readable + writable
+    mappings of this process (contiguous entries may together cover it)."""
+    try:
+        with open(maps_path) as f:
+            lines = f.readlines()
+    except OSError:
+        return False
+    need, end = addr, addr + nbytes
+    spans = []
+    for ln in lines:
+        parts = ln.split()
+        if len(parts) < 2 or not parts[1].startswith("rw"):
+            continue
+        a, b = (int(x, 16) for x in parts[0].split("-"))
+        if b > addr and a < end:
+            spans.append((a, b))
+    for a, b in sorted(spans):
+        if a > need:
+            return False
+        need = max(need, b)
+        if need >= end:
+            return True
+    return False
 
 
 def _store_fence():

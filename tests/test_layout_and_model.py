@@ -88,6 +88,19 @@ def test_fwd_rows_per_block_fills_the_chip_without_a_straggler_wave():
             assert blocks <= FWD_BLOCK_SLOTS
 
 
+@pytest.mark.timeout(20)
+def test_fwd_rows_per_block_terminates_for_many_small_items():
+    """Many items of few rows (large federations' vote / dev scorings): the
+    straggler-wave growth must stop once every item is down to one block
+    (1,100 items and 530 items of ~10 rows looped forever)."""
+    from fedmse_decentralized_amd.ops._hip import fwd_rows_per_block
+
+    for items in (513, 530, 700, 1024, 1100, 1151):
+        for rows_per_item in (1, 10, 64, 100):
+            rpb = fwd_rows_per_block(items * rows_per_item, items)
+            assert rpb % 64 == 0 and rpb >= 64
+
+
 def test_xcd_order_groups_shared_rows_on_one_xcd():
     """Items scoring several models on the same rows (the FedMSE dev set) are
     laid out so every model's block of a row range shares blockIdx % 8 (one
