@@ -35,6 +35,12 @@ import sys
 import tempfile
 import time
 
+from fedmse_decentralized_amd.io.files import reserve_fd_table
+
+# grow the descriptor table while the process is still single-threaded
+# (io.files.reserve_fd_table: later growth waits on RCU in threaded processes)
+reserve_fd_table()
+
 import numpy as np
 import torch
 
@@ -45,23 +51,52 @@ EPISODE = 20   # paper schedule: 20 rounds per run; aggregation caps reset per e
 
 def _collectives_label(comm) -> str:
     """What carries the per-round exchange: RCCL (torch.distributed "nccl"
-    on ROCm), gloo, or nothing (one rank: in-process loopback)."""
+    on ROCm), gloo, or nothing (one rank: in-process loopback).  "xGMI" only
+    when the ranks sit on distinct GPUs (launch.collective_self_test)."""
     if type(comm).__name__ == "PhantomComm":
         return "collectives stubbed: one-GPU projection of rank 0"
+    link = "over xGMI" if getattr(comm, "devices_distinct", False) else "ranks share one GPU"
     if getattr(comm, "active", False):
-        return "peer-memory one-shot all-gather/all-reduce (IPC over xGMI)"
+        return f"peer-memory one-shot all-gather/all-reduce (IPC, {link})"
     try:
         import torch.distributed as dist
 
         if dist.is_available() and dist.is_initialized():
             b = dist.get_backend()
-            return ("RCCL" if b == "nccl" else str(b)) + " all-gather/all-reduce"
+            if b == "nccl":
+                return f"RCCL all-gather/all-reduce ({link})"
+            return f"{b} all-gather/all-reduce"
     except Exception:
         pass
     return "in-process loopback; RCCL all-gather/all-reduce at N > 1"
 
 
+def _spawn_ranks(n: int, argv) -> int:
+    """``python bench.py --gpus N`` without a launcher: start N rank processes
+    through torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) and
+    return their exit code.  Runs before this process touches the GPU; the
+    children inherit stdout, so rank 0's JSON line is this command's output."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    pre.add_argument("--phantom-ranks", type=int, default=0)
+    known, _ = pre.parse_known_args(argv)
+    if known.gpus > 1 and "WORLD_SIZE" not in os.environ and known.phantom_ranks <= 1:
+        return _spawn_ranks(known.gpus, argv)
     # stdout carries exactly ONE line, the JSON record: native libraries'
     # chatter (RCCL prints a version banner to stdout when a communicator is
     # created) is routed to stderr for the duration of the run
@@ -74,6 +109,63 @@ def main(argv=None):
         sys.stdout.flush()
         os.dup2(real_stdout, 1)
         os.close(real_stdout)
+
+
+def _measure(fed, comm, device, steps: int, warmup: int, profile):
+    """Warm-up rounds, then exactly ``steps`` timed rounds bracketed by a
+    barrier + device synchronisation on both sides; every report and artefact
+    of the timed rounds is written before the clock stops.  Returns (seconds,
+    max over ranks; the last RoundResult; per-rank training-launch ms of the
+    timed rounds [ranks, steps] when timed, else None)."""
+    def one_round():
+        if fed.round_idx and fed.round_idx % EPISODE == 0:
+            fed.reset_aggregation_counts()   # new 20-round episode (fresh protocol counters)
+        return fed.run_round()
+
+    for _ in range(warmup):
+        one_round()
+    fed.finish()
+    fed.writer.flush()
+    comm.barrier()
+    if device == "cuda":
+        torch.cuda.synchronize()
+    prof = None
+    if profile and comm.is_root:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
+    fed.tel.reset_totals()   # phase totals cover the timed rounds only
+    fed.writer.mark()
+    r0 = fed.round_idx
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(steps):
+        last = one_round()
+    fed.finish()         # device-protocol rounds: collect results, hand reports to the writer
+    fed.writer.flush()   # artefacts of the timed rounds are on disk before the clock stops
+    if prof is not None:
+        prof.disable()
+        import io
+        import pstats
+
+        s = io.StringIO()
+        pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(40)
+        with open(profile, "w") as f:
+            f.write(s.getvalue())
+    comm.barrier()
+    if device == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # the job is as slow as its slowest rank
+    allt = comm.all_gather(torch.tensor([dt], dtype=torch.float64))
+    dt = float(allt.max())
+    train_ms = None
+    fr = getattr(fed, "_fast", None)
+    if fr is not None and getattr(fr, "train_timing", False):
+        mine = torch.tensor([fr.train_ms.get(r, 0.0) for r in range(r0, r0 + steps)], dtype=torch.float64)
+        train_ms = comm.all_gather(mine).reshape(comm.world_size, steps).numpy()
+    return dt, last, train_ms
 
 
 def _main(argv, real_stdout: int):
@@ -106,6 +198,8 @@ def _main(argv, real_stdout: int):
     p.add_argument("--phantom-ranks", type=int, default=0,
                    help="projection on ONE GPU: run rank 0 of a W-rank weak-scaling job with the collectives "
                         "stubbed out (parallel.comm.PhantomComm); the record is labelled as a projection")
+    p.add_argument("--no-strong", action="store_true",
+                   help="N > 1: skip the extra strong-scaling run of the 10-client federation over the N ranks")
     args = p.parse_args(argv)
 
     from fedmse_decentralized_amd.config import ExperimentConfig
@@ -113,7 +207,6 @@ def _main(argv, real_stdout: int):
     from fedmse_decentralized_amd.parallel.launch import init_comm, shutdown
     from fedmse_decentralized_amd.utils.logging import setup_logging
 
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
     device = "cuda" if torch.cuda.is_available() else "cpu"
     if args.phantom_ranks > 1:
         from fedmse_decentralized_amd.parallel.comm import PhantomComm
@@ -126,63 +219,31 @@ def _main(argv, real_stdout: int):
     if args.gpus != n_gpus and comm.is_root:
         print(f"note: --gpus {args.gpus} but world size is {n_gpus}; using the world size", file=sys.stderr)
     out_root = tempfile.mkdtemp(prefix="fedmx_bench_") if comm.is_root else tempfile.mkdtemp(prefix="fedmx_bench_r")
-    cfg = ExperimentConfig(
-        num_participants=0.5, epoch=args.epochs, num_rounds=10 ** 9, lr_rate=args.lr,
-        shrink_lambda=args.shrink_lambda,
-        network_size=args.clients if args.clients else args.clients_per_gpu * n_gpus, batch_size=args.batch_size,
-        model_types=[args.model_type], update_types=[args.update_type],
-        synthetic=args.data_kind, synthetic_iid=not args.non_iid, compat=args.compat, backend=args.backend,
-        global_early_stop=False, save_checkpoints=not args.no_artifacts, output_root=out_root,
-        trace_file=args.trace, log_level="WARNING")
-    fed = Federation(cfg, args.model_type, args.update_type, run=0, comm=comm,
-                     write_reports=not args.no_artifacts).setup()
-    if args.phantom_ranks > 1 and fed._fast is None:
-        # the host protocol reads other ranks' vote records, which a phantom job does not have
-        raise SystemExit("--phantom-ranks needs the device-resident round protocol (HIP engine, compat fixed)")
-
-    def one_round():
-        if fed.round_idx and fed.round_idx % EPISODE == 0:
-            fed.reset_aggregation_counts()   # new 20-round episode (fresh protocol counters)
-        return fed.run_round()
-
-    for _ in range(args.warmup):
-        one_round()
-    comm.barrier()
-    if device == "cuda":
-        torch.cuda.synchronize()
-    prof = None
-    if args.profile and comm.is_root:
-        import cProfile
-
-        prof = cProfile.Profile()
-        prof.enable()
-    fed.tel.reset_totals()   # phase totals cover the timed rounds only
-    t0 = time.perf_counter()
-    w_busy0 = fed.writer.busy_s
-    last = None
-    for _ in range(args.steps):
-        last = one_round()
-    fed.finish()         # device-protocol rounds: collect results, hand reports to the writer
-    fed.writer.flush()   # artefacts of the timed rounds are on disk before the clock stops
-    if prof is not None:
-        prof.disable()
-        import io
-        import pstats
-
-        s = io.StringIO()
-        pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(40)
-        with open(args.profile, "w") as f:
-            f.write(s.getvalue())
-    comm.barrier()
-    if device == "cuda":
-        torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    # the job is as slow as its slowest rank
-    t = torch.tensor([dt], dtype=torch.float64)
-    allt = comm.all_gather(t)
-    dt = float(allt.max())
-    fed_rps = args.steps / dt
     phantom = args.phantom_ranks > 1
+
+    def build(network_size: int):
+        cfg = ExperimentConfig(
+            num_participants=0.5, epoch=args.epochs, num_rounds=10 ** 9, lr_rate=args.lr,
+            shrink_lambda=args.shrink_lambda, network_size=network_size, batch_size=args.batch_size,
+            model_types=[args.model_type], update_types=[args.update_type],
+            synthetic=args.data_kind, synthetic_iid=not args.non_iid, compat=args.compat, backend=args.backend,
+            global_early_stop=False, save_checkpoints=not args.no_artifacts, output_root=out_root,
+            trace_file=args.trace, log_level="WARNING")
+        fed = Federation(cfg, args.model_type, args.update_type, run=0, comm=comm,
+                         write_reports=not args.no_artifacts).setup()
+        if phantom and fed._fast is None:
+            # the host protocol reads other ranks' vote records, which a phantom job does not have
+            raise SystemExit("--phantom-ranks needs the device-resident round protocol (HIP engine, compat fixed)")
+        return fed
+
+    fed = build(args.clients if args.clients else args.clients_per_gpu * n_gpus)
+    # N > 1: time every rank's training launch (HIP events around it), so the
+    # cost of waiting for the slowest rank's largest client is measured
+    time_train = n_gpus > 1 and fed._fast is not None
+    if time_train:
+        fed._fast.train_timing = True
+    dt, last, train_ms = _measure(fed, comm, device, args.steps, args.warmup, args.profile)
+    fed_rps = args.steps / dt
     # whole-job value: with the default 10 clients per GPU the federation has
     # 10*N clients and the job does N 10-client federations' worth of work
     # per round; for a fixed federation size (--clients) the round rate itself
@@ -198,8 +259,9 @@ def _main(argv, real_stdout: int):
         auc, auc_min = float(np.mean(m)), float(np.min(m))
     else:
         auc = auc_min = float("nan")
+    rec = None
     if comm.is_root:
-        unit = ("rounds/s (10-client-federation equivalents, whole job)" if per_gpu_default
+        unit = ("10-client-federation rounds/s, whole job (= federation rounds/s x clients / 10)" if per_gpu_default
                 else "federation rounds/s")
         rec = {
             "metric": METRIC,
@@ -228,14 +290,26 @@ def _main(argv, real_stdout: int):
                 "local_epochs": args.epochs,
                 "backend": fed.engine.name,
                 "compat": args.compat,
+                "init_mode": fed.cfg.resolved_init_mode(),
                 "device_protocol": fed._fast is not None,
             },
             "federation_rounds_per_sec": round(fed_rps, 4),
             "detection_auc_mean": round(auc, 6),
             "detection_auc_min": round(auc_min, 6),
             "phase_ms_total": {k: round(v, 3) for k, v in fed.tel.summary().items()},
-            "writer_busy_ms_per_round": round(1e3 * (fed.writer.busy_s - w_busy0) / args.steps, 4),
+            "timed_ms": round(1e3 * dt, 3),
+            "writer_busy_ms_per_round": round(1e3 * fed.writer.busy_s_timed / args.steps, 4),
         }
+        if train_ms is not None:
+            t = train_ms                       # [ranks, timed rounds], 0 = no local selection
+            own = t[t > 0]
+            rmax = t.max(axis=0)
+            rec["train_launch_ms"] = {
+                "rank_mean": round(float(own.mean()), 4) if own.size else None,
+                "round_max_mean": round(float(rmax.mean()), 4),
+                "per_rank_mean": [round(float(r[r > 0].mean()), 4) if (r > 0).any() else None for r in t],
+                "note": "HIP-event time of each rank's fused training launch; a round waits for round_max",
+            }
         if phantom:
             # a one-GPU projection, not a multi-GPU measurement: n_gpus stays 1
             # and the whole-job figure goes to projected_value
@@ -244,6 +318,21 @@ def _main(argv, real_stdout: int):
             rec["detection_auc_scope"] = "rank-0 clients only"
             rec["projection"] = (f"rank 0 of a {args.phantom_ranks}-rank job on ONE GPU, collectives stubbed "
                                  "(no RCCL time); projected_value assumes every rank is as fast as this one")
+    if n_gpus > 1 and not phantom and args.clients is None and not args.no_strong:
+        # the same 10-client federation the 1-GPU run measures, now spread over
+        # the N ranks (strong scaling, BASELINE config 4's shape): reported
+        # beside the weak-scaling headline, not folded into it
+        fed.finish()
+        fed10 = build(10)
+        dt10, last10, _ = _measure(fed10, comm, device, args.steps, args.warmup, None)
+        if rec is not None:
+            m10 = np.asarray(last10.metrics, dtype=np.float64)
+            rec["strong_scaling_10_clients"] = {
+                "federation_rounds_per_sec": round(args.steps / dt10, 4),
+                "ms_per_step": round(1e3 * dt10 / args.steps, 4),
+                "detection_auc_mean": round(float(m10.mean()), 6),
+                "detection_auc_min": round(float(m10.min()), 6)}
+    if rec is not None:
         line = json.dumps(rec)
         os.write(real_stdout, (line + "\n").encode())
         if args.out:

@@ -9,8 +9,12 @@ verification, early stop), ``parallel`` (RCCL/gloo/loopback comm, sharding),
 """
 __version__ = "0.1.0"
 
-# grow the descriptor table while the process is (usually) still
-# single-threaded: see io.files.reserve_fd_table
-from .io.files import reserve_fd_table as _reserve_fd_table  # noqa: E402
+# The entry points (main.py, bench.py) grow the descriptor table while the
+# process is still single-threaded (io.files.reserve_fd_table); a library
+# import changes no process-wide state unless FEDMX_RESERVE_FDS=1 asks for it.
+import os as _os
 
-_reserve_fd_table()
+if _os.environ.get("FEDMX_RESERVE_FDS") == "1":
+    from .io.files import reserve_fd_table as _reserve_fd_table
+
+    _reserve_fd_table()

@@ -229,6 +229,10 @@ class DeviceRound:
         self.elect_mode = (1 if cfg.election == "majority" else 0) | (6 if self.thesis else 0)
         self.centralized = cfg.aggregation_mode == "centralized"
         self.pending: deque = deque()
+        # optional: HIP-event time of every round's training launch (bench.py
+        # at N > 1 measures the wait for the slowest rank's largest client)
+        self.train_timing = False
+        self.train_ms: Dict[int, float] = {}
         self.all_rounds: Dict[int, dict] = {}
         self.host_agg_counts = [0] * N
 
@@ -313,7 +317,14 @@ class DeviceRound:
                 ev_std = torch.cuda.Event()
                 ev_std.record(self.side)
         with tel.phase("train"):
+            tev = None
+            if self.train_timing and local_sel:
+                tev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                tev[0].record()
             handle = eng.train_launch(local_rows, fed.hp) if local_sel else None
+            if tev is not None:
+                tev[1].record()
+                rec["train_ev"] = tev
             rec["handle"] = handle
             for c in local_sel:
                 if c in cfg.malicious_clients:   # fault injection: poisoned update (stream-ordered)
@@ -548,6 +559,8 @@ class DeviceRound:
             raise RuntimeError("device AUC reported a class too large for the LDS sort; disable the device "
                                "protocol (--device-protocol false) for this dataset")
         handle = rec.get("handle")
+        if rec.get("train_ev") is not None:
+            self.train_ms[rnd] = rec["train_ev"][0].elapsed_time(rec["train_ev"][1])
         epochs_local: Dict[int, int] = {}
         if handle is not None:
             res = eng.train_collect(handle, [np.array(t) for t in handle.tensors])
@@ -609,6 +622,6 @@ class DeviceRound:
             stop = fed.early.update(float(np.min(metrics)))
         rec.update(aggregator=aggregator, metrics=metrics, verification=verification, epochs_run=epochs_local,
                    stop=stop, done=True)
-        for key in ("handle", "snap_slot", "slot", "report", "_keep", "event", "eval_params", "eval_timing"):
+        for key in ("handle", "snap_slot", "slot", "report", "_keep", "event", "eval_params", "eval_timing", "train_ev"):
             rec.pop(key, None)
         self.all_rounds.pop(rnd, None)

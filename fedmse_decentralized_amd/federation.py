@@ -319,8 +319,9 @@ class Federation:
             selected = select_clients(self.py_rng, N, cfg.num_participants)
             if cfg.dropped_clients:   # fault injection: offline clients neither train, vote nor aggregate
                 selected = [c for c in selected if c not in cfg.dropped_clients]
-            if self._fast is not None:
-                return self._fast.enqueue(selected)
+        if self._fast is not None:
+            return self._fast.enqueue(selected)
+        with self.tel.phase("select"):
             local_sel = [c for c in selected if self._mine(c)]
             local_rows = [self._loc(c) for c in local_sel]
 

@@ -34,6 +34,8 @@ class AsyncWriter:
         self.errors = []
         self.files = ArtifactFiles()   # used only from the job context (writer thread)
         self.busy_s = 0.0   # time spent running jobs (telemetry)
+        self._busy_mark = 0.0
+        self._prev_switch = None
         # FEDMX_WRITER_STATS=1: per job kind (count, seconds), printed by close()
         self.stats = {} if os.environ.get("FEDMX_WRITER_STATS") == "1" else None
         self.jobs = 0
@@ -46,7 +48,9 @@ class AsyncWriter:
             # 5 ms switch interval every such hand-back cost up to 5 ms, which
             # made the writer — not the GPU — bound large federations (64
             # clients: 4.3 ms writer time per round for ~0.2 ms of work).
+            # (restored by close())
             if sys.getswitchinterval() > SWITCH_INTERVAL_S:
+                self._prev_switch = sys.getswitchinterval()
                 sys.setswitchinterval(SWITCH_INTERVAL_S)
             self.t = threading.Thread(target=self._run, name="fedmx-writer", daemon=True)
             self.t.start()
@@ -82,6 +86,14 @@ class AsyncWriter:
             fn()
             return
         self.q.put((event, fn))
+
+    def mark(self) -> None:
+        """Start of a timed region: ``busy_s_timed`` counts job time from here."""
+        self._busy_mark = self.busy_s
+
+    @property
+    def busy_s_timed(self) -> float:
+        return self.busy_s - self._busy_mark
 
     def native_ckpt(self, dims):
         """The process's native checkpoint writer (io.native_writer)."""
@@ -122,6 +134,9 @@ class AsyncWriter:
             self.t.join()
             self.t = None
             self.enabled = False   # a closed writer runs later jobs inline
+            if self._prev_switch is not None:
+                sys.setswitchinterval(self._prev_switch)
+                self._prev_switch = None
         if self.native is not None:
             self.native.close()
             self.native = None

@@ -37,6 +37,7 @@ class Comm:
     device: torch.device = torch.device("cpu")
     phantom: bool = False   # PhantomComm: collectives stubbed (single-GPU projection)
     force_collectives: bool = False
+    devices_distinct: bool = False   # every rank on its own GPU (set by launch.collective_self_test)
 
     @property
     def is_root(self) -> bool:

@@ -79,7 +79,19 @@ class _Channel:
         self.opened: List[int] = []
         areas = [0] * W
         err = 0
+        # ranks on distinct GPUs: the receive areas are read and written over
+        # xGMI, so peer access must be possible before any handle is opened
+        # (ranks sharing a GPU, as in one-box rehearsals, need none)
+        idx = comm.base_all_gather_object(int(comm.device.index))
+        nvis = torch.cuda.device_count()
+        for r in range(W):
+            o = idx[r]
+            if r != me and o != idx[me] and 0 <= o < nvis and not torch.cuda.can_device_access_peer(idx[me], o):
+                err = -2    # no peer access between this GPU and rank r's
+                break
         for r, (_, h) in enumerate(allh):
+            if err:
+                break
             if r == me:
                 areas[r] = self.own
                 continue

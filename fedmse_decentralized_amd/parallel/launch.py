@@ -73,8 +73,58 @@ def init_comm(backend: Optional[str] = None, device: Optional[str] = None, timeo
         # activated collectively by the device protocol's setup_exchange
         from .ipc import IpcComm
 
-        return IpcComm(dev)
-    return TorchDistComm(dev)
+        comm = IpcComm(dev)
+    else:
+        comm = TorchDistComm(dev)
+    if os.environ.get("FEDMX_COMM_SELFTEST", "1") != "0":
+        collective_self_test(comm)
+    return comm
+
+
+def _device_identity(dev: torch.device):
+    """(host, physical GPU) of this rank: ranks on distinct GPUs exchange over
+    xGMI, ranks sharing a GPU (one-box rehearsals) do not."""
+    import socket
+
+    if dev.type != "cuda":
+        return (socket.gethostname(), "cpu", os.getpid())
+    p = torch.cuda.get_device_properties(dev)
+    ident = getattr(p, "uuid", None)
+    ident = str(ident) if ident is not None else f"{os.environ.get('HIP_VISIBLE_DEVICES', '')}:{dev.index}"
+    return (socket.gethostname(), ident)
+
+
+def collective_self_test(comm: Comm) -> dict:
+    """Check the process group right after bring-up, before any federation
+    work: an all-gather of rank-patterned rows and a float64 all-reduce on the
+    rank's device must return exactly the expected values on every rank.  A
+    broken transport (wrong device binding, IPC / dmabuf failure, a rank on
+    the wrong communicator) then fails here with a diagnosis instead of as
+    garbage aggregates or a hang many rounds later.  Also records which
+    ranks share a physical GPU (``comm.devices_distinct``)."""
+    W, r, dev = comm.world_size, comm.rank, comm.device
+    x = torch.arange(257, dtype=torch.float32, device=dev) + 1000.0 * r
+    g = comm.all_gather(x).cpu()
+    want = torch.arange(257, dtype=torch.float32)[None] + 1000.0 * torch.arange(W, dtype=torch.float32)[:, None]
+    s = comm.all_reduce_sum(torch.full((33,), float(r + 1), dtype=torch.float64, device=dev)).cpu()
+    bad_g = (g.shape != want.shape) or not torch.equal(g, want)
+    bad_r = not bool(torch.all(s == W * (W + 1) / 2))
+    ids = comm.all_gather_object(_device_identity(dev))
+    comm.devices_distinct = len(set(ids)) == W
+    comm.peer_devices = ids
+    if bad_g or bad_r:
+        what = []
+        if bad_g:
+            rows = [i for i in range(min(W, g.shape[0])) if not torch.equal(g[i], want[i])]
+            what.append(f"all-gather rows {rows} wrong")
+        if bad_r:
+            what.append(f"all-reduce gave {float(s[0])} (want {W * (W + 1) / 2})")
+        backend = getattr(comm, "backend", "?")
+        msg = (f"[rank {r}/{W}] collective self-test FAILED on {dev} over {backend}: {'; '.join(what)}. "
+               f"Ranks' devices: {ids}. Check one GPU per rank (LOCAL_RANK / HIP_VISIBLE_DEVICES), "
+               "HSA_ENABLE_IPC_MODE_LEGACY=0 for RCCL's dmabuf IPC, and MASTER_ADDR/PORT.")
+        raise RuntimeError(msg)
+    return {"world": W, "devices_distinct": comm.devices_distinct, "devices": ids}
 
 
 def shutdown(comm: Comm) -> None:

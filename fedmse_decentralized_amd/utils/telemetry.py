@@ -49,11 +49,18 @@ class Telemetry:
         self.total: Dict[str, float] = defaultdict(float)
         self.counts: Dict[str, int] = defaultdict(int)
         self.sync = bool(trace_file)
+        self._stack = []
 
     @contextlib.contextmanager
     def phase(self, name: str):
+        """Time a phase.  Phases nest (e.g. ``wait_writer`` inside ``eval``);
+        each is charged its *exclusive* time — a nested phase's time is taken
+        out of its parent's — so the per-phase totals never overlap and sum to
+        at most the wall time they cover."""
         if self.roctx is not None:
             self.roctx.roctxRangePushA(name.encode())
+        frame = [0.0]            # time spent in nested phases
+        self._stack.append(frame)
         t0 = time.perf_counter()
         try:
             yield
@@ -61,10 +68,14 @@ class Telemetry:
             if self.sync and self.sync_fn is not None:
                 self.sync_fn()
             dt = time.perf_counter() - t0
+            self._stack.pop()
+            if self._stack:
+                self._stack[-1][0] += dt
             if self.roctx is not None:
                 self.roctx.roctxRangePop()
-            self.round_times[name] += dt
-            self.total[name] += dt
+            ex = dt - frame[0]
+            self.round_times[name] += ex
+            self.total[name] += ex
             self.counts[name] += 1
 
     def end_round(self, **extra):

@@ -18,6 +18,12 @@ import argparse
 import logging
 import sys
 
+from fedmse_decentralized_amd.io.files import reserve_fd_table
+
+# grow the descriptor table while the process is still single-threaded
+# (io.files.reserve_fd_table: later growth waits on RCU in threaded processes)
+reserve_fd_table()
+
 import torch
 
 from fedmse_decentralized_amd.config import ExperimentConfig, add_arguments, from_args

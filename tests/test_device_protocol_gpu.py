@@ -32,6 +32,25 @@ def _shrink():
         return s
     synthetic.SyntheticSpec.resolved = resolved
     synthetic.SyntheticSpec._fedmx_shrunk = True
+    synthetic.SyntheticSpec._fedmx_orig_resolved = orig
+
+
+class _full_size:
+    """Temporarily undo _shrink (tests whose point is the real client sizes)."""
+
+    def __enter__(self):
+        from fedmse_decentralized_amd.data import synthetic
+
+        self.cls = synthetic.SyntheticSpec
+        self.saved = self.cls.resolved if getattr(self.cls, "_fedmx_shrunk", False) else None
+        if self.saved is not None:
+            self.cls.resolved = self.cls._fedmx_orig_resolved
+        return self
+
+    def __exit__(self, *exc):
+        if self.saved is not None:
+            self.cls.resolved = self.saved
+        return False
 
 
 def _cfg(out, **kw):

@@ -133,10 +133,22 @@ def test_native_async_writer_matches_python_writers(tmp_path):
     w.close()
 
 
-def test_fd_table_reserved_at_import():
-    """Importing the package grows the descriptor table (io.files.reserve_fd_table):
-    a descriptor near the top of the reserved range is usable at once."""
-    import fedmse_decentralized_amd  # noqa: F401
+def test_fd_table_reserved_by_entry_points_not_by_import():
+    """The entry points grow the descriptor table (io.files.reserve_fd_table):
+    a descriptor near the top of the reserved range is usable at once.  A
+    plain package import changes no process-wide state."""
+    import subprocess
+    import sys
+
+    code = ("import resource, fedmse_decentralized_amd; "
+            "print(resource.getrlimit(resource.RLIMIT_NOFILE)[0])")
+    env = dict(os.environ)
+    env.pop("FEDMX_RESERVE_FDS", None)
+    soft = int(subprocess.run([sys.executable, "-c", "import resource; print(resource.getrlimit(resource.RLIMIT_NOFILE)[0])"],
+                              capture_output=True, text=True, env=env).stdout)
+    after = int(subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env,
+                               cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__)))).stdout)
+    assert after == soft
     from fedmse_decentralized_amd.io import files
 
     top = files.reserve_fd_table()

@@ -117,3 +117,27 @@ def test_bench_two_ranks_under_torch_distributed_run():
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["clients"] == 20 and rec["value"] > 0
     assert rec["config"]["parallelism"] == "client-sharded x2 (gloo all-gather/all-reduce)"
+
+
+def test_bench_gpus_flag_spawns_ranks_without_a_launcher():
+    """`python bench.py --gpus 4` with no torch.distributed.run around it
+    starts the 4 rank processes itself (it used to run one rank
+    and report n_gpus 1): one JSON line, n_gpus 4, a 40-client federation,
+    plus the strong-scaling figure of the 10-client federation over 4 ranks."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--backend", "torch",
+                        "--steps", "1", "--warmup", "0", "--epochs", "1", "--no-artifacts"],
+                       cwd=root, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 4 and rec["config"]["clients"] == 40 and rec["value"] > 0
+    assert "x N" not in rec["unit"] and "clients / 10" in rec["unit"]
+    s10 = rec["strong_scaling_10_clients"]
+    assert s10["federation_rounds_per_sec"] > 0 and 0.0 <= s10["detection_auc_mean"] <= 1.0
+    # non-overlapping phase telemetry: the phases sum to at most the timed region
+    assert sum(rec["phase_ms_total"].values()) <= rec["timed_ms"] * 1.001
