@@ -261,6 +261,25 @@ class DeviceRound:
                     vec[self.start + i] = classification_metrics(st.labels(i), s.detach().cpu().numpy())[0]
         return np.asarray(fed.comm.all_reduce_sum(vec), dtype=np.float64)
 
+    def _auc_fallback(self, rec: dict, metrics: np.ndarray) -> np.ndarray:
+        from ..ops import _host
+
+        fed = self.fed
+        bad = np.flatnonzero(metrics == -1.0)
+        vec = np.zeros(self.N, dtype=np.float64)
+        if fed.local:
+            p = fed.engine._plan(fed.model_type, rec["eval_params"])
+            for c in bad:
+                i = int(c) - self.start
+                if 0 <= i < self.n_local:
+                    s = p["scores"][i].detach().double().cpu().numpy()
+                    vec[c] = _host.roc_auc(np.nan_to_num(s), p["labels"][i].cpu().numpy())
+        if fed.comm.collective:
+            vec = np.asarray(fed.comm.all_reduce_sum(vec), dtype=np.float64)
+        out = metrics.copy()
+        out[bad] = vec[bad]
+        return out
+
     def snapshot(self) -> dict:
         """The device-resident protocol state a resumed federation needs
         (aggregation caps, every hosted receiver's verifier history and
@@ -281,6 +300,27 @@ class DeviceRound:
                                  f"this federation needs {tuple(t.shape)}")
             t.copy_(s[k].to(t.device))
         self.host_agg_counts = [int(x) for x in s["host_agg_counts"].tolist()]
+
+    def seed_from_host(self) -> None:
+        """Device protocol state from the federation's host-side state (a
+        resume snapshot written by the host-decision path has no device
+        entry): aggregation caps, and for every hosted receiver its verifier
+        history (the last received aggregate, its performance) and rejection
+        count — what the host path's Verifier would use next."""
+        fed = self.fed
+        self.host_agg_counts = [int(x) for x in fed.agg_counts]
+        self.agg_counts.copy_(torch.tensor(self.host_agg_counts, dtype=torch.int32))
+        for i, c in enumerate(fed.local):
+            vs = fed.vstate.get(c)
+            if vs is None:
+                continue
+            self.rejected[i] = int(vs.rejected_updates)
+            if vs.history_version is not None and vs.history_version in fed.versions:
+                self.hist[i].copy_(fed.versions[vs.history_version])
+                self.has_hist[i] = 1
+                self.hist_perf[i] = float(vs.history_perf)
+            else:
+                self.has_hist[i] = 0
 
     def reset_aggregation_counts(self):
         self.agg_counts.zero_()
@@ -556,8 +596,10 @@ class DeviceRound:
         if cfg.metric != "AUC":
             metrics = self._host_metrics(rec)
         elif bool(np.any(metrics == -1.0)):
-            raise RuntimeError("device AUC reported a class too large for the LDS sort; disable the device "
-                               "protocol (--device-protocol false) for this dataset")
+            # a class too large for the kernel's LDS sort: exact host AUC of
+            # those clients from the round's device scores (the same fallback
+            # as HipEngine._auc_fixup); every rank sees the same set
+            metrics = self._auc_fallback(rec, metrics)
         handle = rec.get("handle")
         if rec.get("train_ev") is not None:
             self.train_ms[rnd] = rec["train_ev"][0].elapsed_time(rec["train_ev"][1])

@@ -213,6 +213,10 @@ class Federation:
             self._fast = DeviceRound(self)
             if snap is not None and snap.get("device"):
                 self._fast.restore(snap["device"])
+            elif snap is not None:
+                # a host-path snapshot resumed on the device path: the device
+                # protocol state starts from the restored host state
+                self._fast.seed_from_host()
         else:
             log.debug(f"device protocol off: {why}")
         return self

@@ -28,10 +28,6 @@ import torch
 from . import _hiprt, build
 
 _lock = threading.Lock()
-# 4: one wave per SIMD (default, fastest measured); 8: two waves per SIMD
-# (fedmx_train8.hip, batch <= 16) — 1.62 ms vs 1.39 ms per 5-client x 5-epoch
-# launch on MI355X (profiles/r1_train8_stamps.txt)
-TRAIN_WAVES = int(os.environ.get("FEDMX_TRAIN_WAVES", "4"))
 # compact internal order of the 4-wave kernel (batch <= 12, hidden <= 27,
 # latent <= 7: padded k-steps skipped); FEDMX_TRAIN_COMPACT=0 forces the
 # identity order (A/B timing, cross-checks)
@@ -141,7 +137,6 @@ def lib():
                 "fedmx_score_reduce_copy": [vp, i32, i32, vp, i32, vp],
                 "fedmx_broadcast_rows": [vp, vp, vp, i32, vp, i32, vp],
                 "fedmx_train": [ctypes.POINTER(TrainArgs), i32, vp],
-                "fedmx_train8": [ctypes.POINTER(TrainArgs), i32, vp],
                 "fedmx_probe_mfma": [vp, vp],
                 "fedmx_elect_wsum": [ctypes.POINTER(ElectArgs), ctypes.POINTER(WsumArgs), vp],
                 "fedmx_decide_adopt": [ctypes.POINTER(DecideArgs), vp],
@@ -660,7 +655,7 @@ class TrainBuffers:
         self.valid_off = torch.from_numpy(store.valid_off).to(dev)
 
 
-def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tensor] = None, waves: int = 0,
+def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tensor] = None,
           compact: Optional[bool] = None, helper: Optional[bool] = None):
     """Launch the fused training kernel for store rows ``local_ids`` (async).
     Returns host views (tracking[k, E, 2], epochs_run[k], best_epoch[k])
@@ -702,11 +697,7 @@ def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tens
     helper_on = TRAIN_HELPER if helper is None else helper
     if helper_on is not None:
         a.flags |= TRAIN_FLAG_HELPER if helper_on else TRAIN_FLAG_NO_HELPER
-    # the 8-wave variant covers single-tile batches only
-    if hp.batch_size <= 16 and (waves or TRAIN_WAVES) == 8:
-        rc = lib().fedmx_train8(ctypes.byref(a), k, rt.stream)
-    else:
-        rc = lib().fedmx_train(ctypes.byref(a), k, rt.stream)
+    rc = lib().fedmx_train(ctypes.byref(a), k, rt.stream)
     if rc == -2:
         raise ValueError(f"fused training kernel needs batch_size >= 1, got {hp.batch_size}")
     _check(rc, "fedmx_train")

@@ -9,9 +9,16 @@
 Both land in ``fedmse_decentralized_amd/ops/lib/`` so they travel with the
 repository snapshot to the GPU box.  ``python -m fedmse_decentralized_amd.ops.build``
 rebuilds what is stale.
+
+Staleness is decided by content, not by file times: every library has a
+``<lib>.buildhash`` stamp next to it holding the SHA-256 of its compiler,
+flags and the bytes of every source and header that goes into it.  A library
+whose stamp is missing or differs is rebuilt (a copied tree with fresh mtimes
+rebuilds nothing; an edited source is never hidden by a newer ``.so``).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -36,11 +43,30 @@ def _headers():
     return sorted(p for p in CSRC.rglob("*") if p.suffix in (".h", ".hpp", ".cuh", ".inc"))
 
 
-def _stale(target: Path, deps) -> bool:
-    if not target.exists():
+def _hash_path(target: Path) -> Path:
+    return target.with_name(target.name + ".buildhash")
+
+
+def content_hash(cmd, deps) -> str:
+    """SHA-256 over the compile command (sans output path) and every input's
+    name and bytes, in a fixed order."""
+    h = hashlib.sha256()
+    h.update("\0".join(map(str, cmd)).encode())
+    for p in sorted(set(deps), key=lambda q: q.relative_to(CSRC).as_posix()):
+        h.update(b"\0" + p.relative_to(CSRC).as_posix().encode() + b"\0")
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+def _stale(target: Path, digest: str) -> bool:
+    hp = _hash_path(target)
+    if not target.exists() or not hp.exists():
         return True
-    t = target.stat().st_mtime
-    return any(p.stat().st_mtime > t for p in deps)
+    return hp.read_text().strip() != digest
+
+
+def _stamp(target: Path, digest: str) -> None:
+    _hash_path(target).write_text(digest + "\n")
 
 
 def _run(cmd, cwd=None):
@@ -52,15 +78,17 @@ def _run(cmd, cwd=None):
 
 def build_host(force: bool = False, verbose: bool = False) -> Path:
     srcs = _sources("host", (".cpp",))
-    if not force and not _stale(HOST_LIB, srcs + _headers()):
+    cxx = os.environ.get("CXX", "g++")
+    flags = [cxx, "-std=c++17", "-O3", "-fPIC", "-shared", "-pthread", "-Wall"]
+    digest = content_hash(flags + [p.name for p in srcs], srcs + _headers())
+    if not force and not _stale(HOST_LIB, digest):
         return HOST_LIB
     LIBDIR.mkdir(parents=True, exist_ok=True)
-    cxx = os.environ.get("CXX", "g++")
     tmp = HOST_LIB.with_suffix(".so.tmp")
-    cmd = [cxx, "-std=c++17", "-O3", "-fPIC", "-shared", "-pthread", "-Wall",
-           *map(str, srcs), "-o", str(tmp)]
+    cmd = flags + [*map(str, srcs), "-o", str(tmp)]
     out = _run(cmd)
     os.replace(tmp, HOST_LIB)
+    _stamp(HOST_LIB, digest)
     if verbose:
         print(out, end="")
     return HOST_LIB
@@ -78,21 +106,22 @@ def build_hip(force: bool = False, verbose: bool = False, extra_flags=(), target
     the in-kernel timestamp build ``-DFEDMX_STAMPS=1`` -> ``libfedmx_hip_stamps.so``
     (selected at load time with ``FEDMX_HIP_LIB``)."""
     srcs = _sources("hip", (".hip",))
-    if not force and not _stale(target, srcs + _headers()):
-        return target
-    LIBDIR.mkdir(parents=True, exist_ok=True)
-    tmp = target.with_suffix(".so.tmp")
     # -ffp-contract=off: separately rounded mul/add like the torch ops the kernels
     # reproduce (aggregation sums are then bit-identical to the reference order)
     # -amdgpu-mfma-vgpr-form: MFMA accumulators in arch VGPRs (the training
     # kernel otherwise pays ~150 v_accvgpr moves per step on its VALU-bound
     # optimizer tail: -3.3% launch time measured)
-    cmd = [hipcc_path(), f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-munsafe-fp-atomics", "-mllvm", "-amdgpu-mfma-vgpr-form=1",
-           f"-I{CSRC / 'hip'}", *extra_flags, *map(str, srcs),
-           "-o", str(tmp)]
+    flags = [f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+             "-ffp-contract=off", "-munsafe-fp-atomics", "-mllvm", "-amdgpu-mfma-vgpr-form=1", *extra_flags]
+    digest = content_hash(["hipcc", *flags, *(p.name for p in srcs)], srcs + _headers())
+    if not force and not _stale(target, digest):
+        return target
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    tmp = target.with_suffix(".so.tmp")
+    cmd = [hipcc_path(), *flags, f"-I{CSRC / 'hip'}", *map(str, srcs), "-o", str(tmp)]
     out = _run(cmd)
     os.replace(tmp, target)
+    _stamp(target, digest)
     if verbose:
         print(out, end="")
     return target

@@ -1,5 +1,5 @@
 // Shared pieces of the fused local-training kernels (fedmx_train.hip: 4 waves,
-// fedmx_train8.hip: 8 waves): kernel arguments, the fused Adam update, the
+// fedmx_train_hw.hip: 4 main + 4 helper waves): kernel arguments, the fused Adam update, the
 // in-kernel timestamp macro and the dense <-> LDS-master parameter staging.
 #pragma once
 #include "fedmx_common.h"
@@ -33,7 +33,7 @@ struct TrainArgs {
   int32_t* best_epoch;      // [k]
   int32_t epochs, batch, patience, d_in, hidden, latent;
   float lr, beta1, beta2, eps, lambda, mu;
-  uint64_t* stamps;         // [4 waves][32] s_memtime stamps of one step (FEDMX_STAMPS builds), or null
+  uint64_t* stamps;         // [8 waves][32] s_memtime stamps of one step (FEDMX_STAMPS builds), or null
   int32_t flags;            // TRAIN_FLAG_* bits
   int32_t pad0;
 };

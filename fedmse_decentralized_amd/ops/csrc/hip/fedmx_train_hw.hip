@@ -41,6 +41,20 @@
 namespace fedmx {
 namespace hw {
 
+// In-kernel phase stamps (-DFEDMX_STAMPS=1 builds, scripts/train_stamps.py):
+// row w8 (0..7: mains then helpers) of A.stamps, columns as in fedmx_train.hip.
+#if FEDMX_STAMPS
+#define HSTAMP(cond, i)                                                                         \
+  do {                                                                                          \
+    if ((cond) && A.stamps != nullptr && blockIdx.x == 0 && lane == 0)                          \
+      A.stamps[w8 * 32 + (i)] = __builtin_amdgcn_s_memtime();                                  \
+  } while (0)
+#else
+#define HSTAMP(cond, i) \
+  do {                  \
+  } while (0)
+#endif
+
 constexpr int L_W1 = HP * S_W1;          // 4224
 constexpr int L_W4 = DP * S_W4;          // 4608
 constexpr int L_W2 = ZP * S_W2;          // 576
@@ -391,9 +405,16 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // w8 takes batches w8, w8+8, ...), fixed-order loss exchange, tracking,
   // patience decision, best-validation snapshot.  True: stop training.
   auto epoch_tail = [&](int ep, double acc_tr, double prox_now) -> bool {
+    HSTAMP(ep == 0, 12);
     __syncthreads();   // masters published (W1 by mains, W4 by helpers, small tiles)
     double acc_va = 0.0;
-    for (int vt = w8; vt < nvt; vt += 8) valid_chunk(Xva, 16 * vt, n_va, acc_va);
+    HSTAMP(ep == 0, 14);
+    for (int vt = w8; vt < nvt; vt += 8) {
+      HSTAMP(ep == 0 && vt == w8, 16);
+      valid_chunk(Xva, 16 * vt, n_va, acc_va);
+      HSTAMP(ep == 0 && vt == w8, 17);
+    }
+    HSTAMP(ep == 0, 15);
     {
       const double s0 = wave_sum_d(acc_tr);
       const double s1 = wave_sum_d(acc_va);
@@ -430,11 +451,13 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       ++worse;
     }
     __syncthreads();   // sLoss reuse / masters stable for the snapshot copy
+    HSTAMP(ep == 0, 13);
     return worse >= A.patience && worse > 0;
   };
   // prologue staging: the stagers issue the loads of every state tensor
   // (m, v, [anchor], params) in one memory round trip, then each tensor
   // passes through the masters in turn (the barrier sequence of one global_to_masters_o pass per tensor)
+  HSTAMP(true, 28);
   f32x4 pv_m[STAGE_PER_THREAD], pv_v[STAGE_PER_THREAD], pv_a[STAGE_PER_THREAD], pv_p[STAGE_PER_THREAD];
   if (stager) {
     stage_load(Mg, pv_m);
@@ -486,8 +509,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       double acc_tr = 0.0;
       // W4 gradient + Adam between barrier #2 of step s and barrier #1 of s+1
       for (int bi = 0; bi < nb; ++bi) {
+        const bool hs = (ep == 0 && bi == STAMP_STEP);
+        HSTAMP(hs, 0);
         __syncthreads();   // barrier #1 (main: layer-1 partials)
+        HSTAMP(hs, 2);
         __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
+        HSTAMP(hs, 7);
         const f32x4 w4a0 = lds_read4(sT0 + tr);
         const f32x4 w4a1 = lds_read4(sT0 + tr + 16 * S_T);
         const f32x4 w4b0 = lds_read4(sT1 + tr);
@@ -504,6 +531,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           G4[1][0] = mfma16(w4a1[s], w4b0[s], G4[1][0]);
           G4[1][1] = mfma16(w4a1[s], w4b1[s], G4[1][1]);
         }
+        HSTAMP(hs, 8);
         float prox_acc = 0.f;
 #pragma unroll
         for (int v = 0; v < 2; ++v)
@@ -511,12 +539,14 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           for (int t = 0; t < 2; ++t)
             adam4<PROX>(P4.q4[v][t], M4.q4[v][t], V4.q4[v][t], AN4.q4[v][t], G4[v][t], K, prox_acc);
         if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
+        HSTAMP(hs, 10);
         // publish W4(s+1): master rows (layer 4, validation, snapshots) and the
         // dH3 A-operand copy; main w reads both after barrier #1 of step s+1
         w4_to_lds(P4, L);
         publish_q4();
         ++js;
         publish_k();   // step js's scalars, read by the mains after its barrier #1
+        HSTAMP(hs, 11);
       }
       double prox_now = 0.0;
       if (PROX) {
@@ -542,6 +572,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     __syncthreads();
     w4_to_lds(V4, L);
     __syncthreads();
+    HSTAMP(true, 31);
     return;
   }
 
@@ -563,6 +594,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   }
   stage_vals(pv_p);
   lds_to_mslab(P, L);   // W2/W3/W4 masters stay live; W1 lives in registers only
+  HSTAMP(true, 29);
 
   auto l1_partial = [&](const XChunk& x, f32x4& acc0, f32x4& acc1) {
     acc0 = zero4();
@@ -595,6 +627,8 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       const int row_n = (bi + 1) * B;
       const int bc_n = has_next ? min(B, n_tr - row_n) : 0;
       const float inv_bt = 1.0f / (float)bt;
+      const bool ms = (ep == 0 && bi == STAMP_STEP);
+      HSTAMP(ms, 0);
       f32x4 G1[2][2], Go = zero4();
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -608,7 +642,9 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         float* red = sRedH1 + parity * L_RED;
         lds_write4(red + (w * 2 + 0) * 256 + lane * 4, l1a);
         lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1b);
+        HSTAMP(ms, 1);
         __syncthreads();  // barrier #1
+        HSTAMP(ms, 2);
         {
           // this step's Adam scalars (helper-published)
           const f32x4 kk = lds_read4(sK + 4 * (js & 1));
@@ -701,6 +737,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         float contrib = sq * (inv_bt * inv_d);
         if (w == 0 && g == 0 && col_ok) contrib += lam * norm_c * inv_bt;
         if (!(FEDMX_HW_ABLATE & 2)) acc_tr += (double)contrib;
+        HSTAMP(ms, 3);
       }
       if (has_next) load_chunk(Xtr, row_n, bc_n, nxt);  // prefetch
 
@@ -745,7 +782,9 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         sH1T[tw + (16 + r) * S_T] = h1[1][r];
         sZT[tw + r * S_T] = zb[r];
       }
+      HSTAMP(ms, 4);
       __syncthreads();  // barrier #2: dH3 partials of all waves visible
+      HSTAMP(ms, 7);
       f32x4 dh3[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -787,6 +826,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         for (int r = 0; r < 4; ++r) acc[r] = (hreal_c[t] && h1b[t][r] > 0.f) ? acc[r] : 0.f;
         dh1b[t] = acc;
       }
+      HSTAMP(ms, 8);
       // ---- dW1^T (own columns) = X^T dH1
 #pragma unroll
       for (int s = 0; s < KB; ++s) {
@@ -804,17 +844,20 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
         for (int s = 0; s < KB; ++s) Go = mfma16(a[s], b[s], Go);
       }
+      HSTAMP(ms, 9);
       // W1 first: the next chunk's layer-1 product waits on it
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int v = 0; v < 2; ++v) adam4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
+      HSTAMP(ms, 10);
       // (after an epoch's last batch this works on a stale tile; unused)
       finalize_chunk(nxt);
       l1_partial(nxt, l1a, l1b);
       if (!(FEDMX_HW_ABLATE & 4)) adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
       if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
       if (!(FEDMX_HW_ABLATE & 4)) own_to_lds(P, L);   // read by every wave after barrier #1
+      HSTAMP(ms, 11);
       __builtin_amdgcn_iglp_opt(0);
       cur = nxt;
     }
@@ -842,6 +885,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   }
 
   // ---- write back: params (masters), then m and v through the same staging
+  HSTAMP(true, 30);
   __syncthreads();
   masters_to_global_o<CP>(Pg, sW1, sW4, sW2, sW3);
   __syncthreads();
@@ -854,6 +898,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   own_to_lds(V, L);
   __syncthreads();
   masters_to_global_o<CP>(Vg, sW1, sW4, sW2, sW3);
+  HSTAMP(true, 31);
   if (threadIdx.x == 0) {
     A.adam_step[cid] = step;
     A.epochs_run[kslot] = ep_run;

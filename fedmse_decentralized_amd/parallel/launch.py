@@ -77,7 +77,13 @@ def init_comm(backend: Optional[str] = None, device: Optional[str] = None, timeo
     else:
         comm = TorchDistComm(dev)
     if os.environ.get("FEDMX_COMM_SELFTEST", "1") != "0":
-        collective_self_test(comm)
+        res = collective_self_test(comm)
+        if comm.is_root:
+            import sys
+
+            print(f"collective self-test ok: {res['world']} rank(s) over {getattr(comm, 'backend', '?')}, "
+                  f"devices {'distinct' if res['devices_distinct'] else 'shared'}: {res['devices']}",
+                  file=sys.stderr)
     return comm
 
 

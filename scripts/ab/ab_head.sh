@@ -2,7 +2,7 @@
 # Build the committed (HEAD) kernels as libfedmx_hip_head.so next to the
 # working-tree library, for a same-box A/B with scripts/ab_train.sh.
 set -eu
-ROOT=$(cd "$(dirname "$0")/.." && pwd)
+ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 TMP=$(mktemp -d)
 git -C "$ROOT" archive HEAD fedmse_decentralized_amd/ops/csrc | tar -x -C "$TMP"
 python - "$ROOT" "$TMP" <<'PY'

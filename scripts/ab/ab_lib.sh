@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B two builds of the HIP library on the training-kernel microbenchmark:
-#   bash scripts/ab_lib.sh <alt .so path>
+#   bash scripts/ab/ab_lib.sh <alt .so path>
 set -u
 OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out
 mkdir -p "$OUT"

@@ -54,7 +54,7 @@ VARIANTS = {
     "s_norp": ["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule=1"],  # 957.4 / 961.0
     "s_bias0": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],                # 947.1 / 945.3
     "s_cyc": ["-mllvm", "-misched-cyclicpath=1"],                           # 946.7 / 945.9
-    # fused verification kernel, timing-only (r2, base 24.6 us; scripts/r2_verify_ablate.sh)
+    # fused verification kernel, timing-only (r2, base 24.6 us; scripts/ab/r2_verify_ablate.sh)
     "vabl1": ["-DFEDMX_VERIFY_ABLATE=1"],         # no forward                13.4 us
     "vabl2": ["-DFEDMX_VERIFY_ABLATE=2"],         # no drift                  18.9 us
     "vabl4": ["-DFEDMX_VERIFY_ABLATE=4"],         # no adoption pass          21.4 us

@@ -21,7 +21,7 @@ step() {  # name seconds cmd...
 MODE=${1:-all}
 python -c "import fedmse_decentralized_amd.ops.build as b; b.build_all()" || exit 3
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-  step pytest_gpu 420 python -m pytest tests -m gpu -x -q
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
   step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = kernels ]; then
@@ -30,6 +30,11 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 300 python bench.py --steps 50 --warmup 5 --out "$OUT/bench.json"
   step bench_cprofile 300 python bench.py --steps 20 --warmup 3 --out "$OUT/bench_cprofile.json" --profile "$OUT/bench_profile.txt"
+fi
+if [ "$MODE" = all ] || [ "$MODE" = rccl1 ]; then
+  # the multi-GPU code path over a real one-rank RCCL group (prints the collective self-test)
+  step rccl1 300 env FEDMX_FORCE_COLLECTIVES=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+    --master-addr 127.0.0.1 --master-port 29533 bench.py --steps 50 --warmup 5 --out "$OUT/bench_rccl1.json"
 fi
 if [ "$MODE" = stamps ]; then
   step train_stamps 300 python scripts/train_stamps.py

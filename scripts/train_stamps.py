@@ -1,9 +1,14 @@
 """In-kernel phase timing of the fused training kernel (s_memtime stamps).
 
 Loads the ``-DFEDMX_STAMPS=1`` build (``libfedmx_hip_stamps.so``), trains the
-flagship round's 5 clients once and prints, per wave, the cycles spent in each
-phase of one training step (epoch 0, step STAMP_STEP), of one validation
-batch, and of the launch prologue / epilogue.
+flagship round's 5 clients once and prints, per wave, the counter ticks spent
+in each phase of one training step (epoch 0, step STAMP_STEP), of one
+validation tile, and of the launch prologue / epilogue.  The default kernel
+for the reference shapes is the helper-wave kernel (``fedmx_train_hw.hip``:
+waves 0-3 run the step's chain, 4-7 the W4 gradient + Adam); ``--four-waves``
+stamps the 4-wave kernel (``fedmx_train.hip``) instead.  ``--json out`` also
+writes every repetition's table.  s_memtime counts at a fixed reference
+clock (100 MHz on gfx9 parts: 1 tick = 10 ns); ``--ticks-per-us`` overrides.
 """
 from __future__ import annotations
 
@@ -28,7 +33,7 @@ from fedmse_decentralized_amd.models.layout import DEFAULT_DIMS  # noqa: E402
 from fedmse_decentralized_amd.models.reference import init_client_params  # noqa: E402
 from fedmse_decentralized_amd.ops import _hip, build  # noqa: E402
 
-PHASES = [
+PHASES4 = [
     (0, 1, "L1 partial write"), (1, 2, "barrier #1"), (2, 3, "fwd reduce + L2..L4 + loss"),
     (3, 4, "prefetch + dY/transposes + dH3 partial + stage"), (4, 5, "dW4 mfma"),
     (6, 7, "barrier #2"), (7, 8, "dH3 reduce + dZ + dH1 (batch-major)"), (8, 9, "dW1 mfma + small tile"),
@@ -37,6 +42,20 @@ PHASES = [
     (28, 29, "prologue (state load)"),
     (12, 13, "epoch end (reduce + snapshot)"), (30, 31, "epilogue (write back)"),
 ]
+# helper-wave kernel: rows 0-3 = main waves, 4-7 = helpers (fedmx_train_hw.hip HSTAMP points)
+PHASES_HW = [
+    (0, 1, "main: L1 partial write"), (1, 2, "main: barrier #1 wait"),
+    (2, 3, "main: L1 reduce + L2..L4 + loss"), (3, 4, "main: prefetch + dY + dH3 partial + stage"),
+    (4, 7, "main: barrier #2 wait"), (7, 8, "main: dH3 reduce + dZ + dH1"),
+    (8, 9, "main: dW1 + small-tile MFMAs"), (9, 10, "main: adam W1"),
+    (10, 11, "main: next L1 + adam small + publish"), (0, 11, "main: STEP (stamp 0 -> 11)"),
+    (0, 2, "helper: barrier #1 wait"), (2, 7, "helper: barrier #2 wait"), (7, 8, "helper: dW4 MFMAs"),
+    (8, 10, "helper: adam W4"), (10, 11, "helper: publish W4 + scalars"),
+    (16, 17, "valid: one 16-row tile (one wave)"), (14, 15, "valid: epoch pass (per wave)"),
+    (12, 13, "epoch tail (barriers, validation, exchange, snapshot)"),
+    (28, 29, "prologue (state load, mains)"), (30, 31, "epilogue (write back, mains)"),
+]
+FOUR = "--four-waves" in sys.argv
 
 
 def main():
@@ -51,25 +70,32 @@ def main():
               [c.test_label for c in clients], init)
     hp = TrainHParams(epochs=5, batch_size=12, lr=1e-3, shrink_lambda=5.0, patience=10 ** 6)
     stamps = torch.zeros(8 * 32, dtype=torch.int64, device=dev)
-    nw = 8 if (_hip.TRAIN_WAVES == 8) else 4
+    helper = not FOUR
+    nw = 8 if helper else 4
+    phases = PHASES_HW if helper else PHASES4
     if PLAIN:
         for _ in range(3):
-            _hip.train(eng.store, list(range(5)), hp, eng.dims)
+            _hip.train(eng.store, list(range(5)), hp, eng.dims, helper=helper)
         torch.cuda.synchronize()
         print("plain train launches done")
         return
     out = {}
-    for rep in range(3):
-        _hip.train(eng.store, list(range(5)), hp, eng.dims, stamps=stamps)
+    for rep in range(4):
+        _hip.train(eng.store, list(range(5)), hp, eng.dims, stamps=stamps, helper=helper)
         torch.cuda.synchronize()
         st = stamps.view(8, 32).cpu().numpy().astype(np.int64)[:nw]
         res = {}
-        for a, b, name in PHASES:
+        for a, b, name in phases:
             res[name] = [int(st[w, b] - st[w, a]) if st[w, a] and st[w, b] else None for w in range(nw)]
         out[f"rep{rep}"] = res
         stamps.zero_()
-    for name, v in out["rep2"].items():
-        print(f"{name:34s} " + " ".join(f"{x:8d}" if x is not None else "       -" for x in v))
+    last = out[f"rep{len(out) - 1}"]
+    print(f"{'phase (ticks, rep ' + str(len(out) - 1) + ')':52s} " + " ".join(f"{'w' + str(w):>6s}" for w in range(nw)))
+    for name, v in last.items():
+        print(f"{name:52s} " + " ".join(f"{x:6d}" if x is not None else "     -" for x in v))
+    if "--json" in sys.argv:
+        with open(sys.argv[sys.argv.index("--json") + 1], "w") as f:
+            json.dump(out, f)
     print(json.dumps(out))
 
 

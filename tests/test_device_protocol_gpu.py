@@ -274,6 +274,64 @@ def test_device_round_resume_matches_uninterrupted(tmp_path):
         assert torch.equal(getattr(a._fast, name), getattr(b._fast, name)), name
 
 
+def test_device_round_auc_with_a_class_beyond_the_lds_sort(tmp_path):
+    """Clients whose test classes both exceed the AUC kernel's 8,192-key LDS
+    sort (~9,000 benign and ~10,000 attack rows): the device protocol falls back to the exact
+    host AUC for them instead of failing, and reports the host
+    path's metrics."""
+    from fedmse_decentralized_amd.data import synthetic
+
+    cls = synthetic.SyntheticSpec
+    saved = cls.resolved
+    base = getattr(cls, "_fedmx_orig_resolved", saved)
+
+    def big(self):
+        s = base(self)
+        # both test classes beyond the sort (the kernel sorts the smaller one)
+        s.normal_rows, s.abnormal_rows, s.test_normal_rows = (150, 170), (10000, 10040), 9000
+        return s
+    cls.resolved = big
+    try:
+        fa, a = _run(_cfg(str(tmp_path / "dev"), save_checkpoints=False, network_size=4), "mse_avg", 3)
+        fb, b = _run(_cfg(str(tmp_path / "host"), save_checkpoints=False, network_size=4, device_protocol=False),
+                     "mse_avg", 3)
+    finally:
+        cls.resolved = saved
+    assert fa._fast is not None and fb._fast is None
+    lab = fa.engine.store.labels(0)
+    assert min(int(lab.sum()), int((lab == 0).sum())) > 8192
+    assert a == b
+    assert all(0.5 < m <= 1.0 for ms in a["metrics"] for m in ms)
+
+
+def test_host_snapshot_resumed_on_device_path(tmp_path):
+    """A resume snapshot written by the host-decision path (no device entry)
+    resumed with the device protocol: the device state is seeded from the
+    restored host state (caps, verifier histories, rejection counts), so the
+    resumed rounds equal the uninterrupted host-path run's."""
+    _shrink()
+    from fedmse_decentralized_amd import federation
+    from fedmse_decentralized_amd.federation import Federation
+
+    federation._PREP_CACHE.clear()
+    a = Federation(_cfg(str(tmp_path / "a"), save_checkpoints=False, device_protocol=False), "hybrid", "mse_avg",
+                   0).setup()
+    assert a._fast is None
+    for _ in range(3):
+        a.run_round()
+    snap = a.save_snapshot(str(tmp_path / "snap.pt"))
+    ra = [a.run_round() for _ in range(3)]
+    ra = [(r.aggregator, r.verification) for r in ra]
+    federation._PREP_CACHE.clear()
+    b = Federation(_cfg(str(tmp_path / "b"), save_checkpoints=False, resume=snap), "hybrid", "mse_avg", 0).setup()
+    assert b._fast is not None and b.round_idx == 3
+    rb = [b.run_round() for _ in range(3)]
+    b.finish()
+    rb = [(r.aggregator, r.verification) for r in rb]
+    assert ra == rb
+    torch.testing.assert_close(a.engine.store.params, b.engine.store.params, rtol=0, atol=0)
+
+
 def test_device_round_save_latents_matches_host_path(tmp_path):
     """--save-latents (LatentData pickles) on the device-resident
     protocol: the same per-round test-set latents as the host path."""
@@ -417,7 +475,10 @@ def _worker_kw(rank, world, port, out, kw):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("kw", [dict(protocol_variant="thesis", election="majority"),
                                 dict(metric="classification", fedavg_sample_weighted=True),
-                                dict(aggregation_mode="centralized", dropped_clients=[2])])
+                                dict(aggregation_mode="centralized", dropped_clients=[2]),
+                                # poisoned updates: receivers on both ranks reject, and every
+                                # side slot is reused (4 rounds > 3 slots) with fresh counts
+                                dict(malicious_clients=[1, 4], malicious_scale=25.0)])
 def test_device_round_variants_multi_rank_one_gpu(tmp_path, kw):
     """Protocol variants on the device path with two gloo ranks sharing one
     GPU: every rank reaches the single-process run's decisions, metrics and

@@ -257,21 +257,6 @@ def test_train_kernel_many_clients_concurrently():
     assert torch.equal(hip.store.params[untouched].cpu(), canonical_to_padded(init[untouched]))
 
 
-@pytest.mark.parametrize("lam,mu", [(5.0, 0.0), (5.0, 0.001)])
-def test_train8_kernel_matches_torch_engine(lam, mu):
-    """The opt-in 8-wave (two waves per SIMD) training kernel."""
-    ref, hip = _setup_pair()
-    hp = TrainHParams(epochs=3, batch_size=12, lr=1e-3, shrink_lambda=lam, fedprox_mu=mu, patience=1)
-    r1 = ref.train([0, 1], hp)
-    trk, er, be = _hip.train(hip.store, [0, 1], hp, hip.dims, waves=8)
-    torch.cuda.synchronize()
-    _hip.runtime(DEV).sync()
-    assert list(r1.epochs_run) == [int(x) for x in er]
-    torch.testing.assert_close(hip.store.params.cpu(), ref.store.params, rtol=2e-3, atol=2e-5)
-    torch.testing.assert_close(hip.store.best.cpu(), ref.store.best, rtol=2e-3, atol=2e-5)
-    assert torch.equal(hip.store.adam_step.cpu(), ref.store.adam_step)
-
-
 def test_copy_rows_gather_scatter():
     """Row copies through mapped index arrays (multi-rank exchange packing)."""
     rt = _hip.runtime(DEV)

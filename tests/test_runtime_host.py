@@ -17,3 +17,30 @@ def test_cpu_mapping_check_sees_host_buffers_and_rejects_unmapped(tmp_path):
     assert not _hiprt._cpu_mapped_rw(0x28000, 0x10000, str(maps))   # hole 30000-40000
     assert not _hiprt._cpu_mapped_rw(0x48000, 0x10000, str(maps))   # read-only tail
     assert not _hiprt._cpu_mapped_rw(0x18000, 16, str(tmp_path / "missing"))
+
+
+def test_build_staleness_is_content_based(tmp_path):
+    """ops/build.py decides staleness by a hash of compiler flags and source
+    bytes stored next to the library (mtime-based staleness could
+    silently reuse a pushed .so newer than an edited source)."""
+    import os
+
+    from fedmse_decentralized_amd.ops import build
+
+    srcs = build._sources("hip", (".hip",)) + build._headers()
+    d1 = build.content_hash(["hipcc", "-O3"], srcs)
+    assert d1 == build.content_hash(["hipcc", "-O3"], list(reversed(srcs)))   # order-independent
+    assert d1 != build.content_hash(["hipcc", "-O2"], srcs)                   # flags count
+    lib = tmp_path / "libx.so"
+    assert build._stale(lib, d1)                     # no library
+    lib.write_bytes(b"\x7fELF")
+    assert build._stale(lib, d1)                     # no stamp
+    build._stamp(lib, d1)
+    assert not build._stale(lib, d1)
+    os.utime(lib, (0, 0))                            # file times play no part
+    assert not build._stale(lib, d1)
+    assert build._stale(lib, "0" * 64)               # any source / flag change
+    # the in-tree libraries carry their stamps after build()
+    for target in (build.HOST_LIB, build.HIP_LIB):
+        if target.exists() and build._hash_path(target).exists():
+            assert len(build._hash_path(target).read_text().strip()) == 64
