@@ -33,6 +33,23 @@
 #ifndef FEDMX_HW_ABLATE
 #define FEDMX_HW_ABLATE 0
 #endif
+// dH3 partial reads: 0 = read-add per partial (the compiler serialised them
+// into six LDS round trips), 1 = all eight reads first, 2 = same + a
+// scheduling fence after the reads
+#ifndef FEDMX_HW_REDUCE
+#define FEDMX_HW_REDUCE 2
+#endif
+// 1: the helpers form step s+1's Adam scalars (an f64 dependency chain) in
+// their idle window between barriers #1 and #2 of step s instead of right
+// before barrier #1, where they sat on the helpers' path
+#ifndef FEDMX_HW_KEARLY
+#define FEDMX_HW_KEARLY 1
+#endif
+// bias column of X: 1 = the bias lanes load from kBiasX (address select),
+// 0 = overwrite the loaded registers (finalize)
+#ifndef FEDMX_HW_BIASX
+#define FEDMX_HW_BIASX 1
+#endif
 // issue priority of the main waves over their helpers (s_setprio level; 0: equal)
 #ifndef FEDMX_HW_PRIO
 #define FEDMX_HW_PRIO 0
@@ -138,6 +155,10 @@ struct XChunk {
   f32x4 f0, f1, b0, b1;
 };
 
+// what the bias lane reads for X's last four columns (padding, padding,
+// padding, the constant-1 bias column)
+__device__ __attribute__((aligned(16))) const float kBiasX[4] = {0.f, 0.f, 0.f, 1.f};
+
 template <bool PROX>
 __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   constexpr bool CP = true;
@@ -235,21 +256,27 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) brow_b[r] = batch_row_of_col<CP>(4 * g + r);
 
+  // The bias column DP-1 of X reads as 1 (it feeds W1a's b1 column): the
+  // lanes that hold it load from kBiasX instead of X.  Selecting the address
+  // (not overwriting the loaded register) leaves nothing that waits on the
+  // prefetch before its first real use: a post-load select was hoisted by the
+  // scheduler into the forward and stalled it on the prefetch every step.
   auto load_chunk = [&](const float* X, int row0, int bc, XChunk& x) {
     const float* src = X + (size_t)(row0 + ((unsigned)brow_c < (unsigned)bc ? brow_c : 0)) * DP + xcol;
     x.f0 = *reinterpret_cast<const f32x4*>(src);
-    x.f1 = *reinterpret_cast<const f32x4*>(src + 16);
+    x.f1 = *reinterpret_cast<const f32x4*>(FEDMX_HW_BIASX && bias_lane ? kBiasX : src + 16);   // cols DP-4..DP-1
     const float* bsrc = X + (size_t)row0 * DP + 32 * w + c;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {   // row quad 3 is padding, never read
       const int rr = ((unsigned)brow_b[r] < (unsigned)bc) ? brow_b[r] : 0;
       x.b0[r] = bsrc[(size_t)rr * DP];
-      x.b1[r] = bsrc[(size_t)rr * DP + 16];
+      x.b1[r] = *(FEDMX_HW_BIASX && bias_col ? kBiasX + 3 : bsrc + (size_t)rr * DP + 16);
     }
     x.b0[3] = 0.f;
     x.b1[3] = 0.f;
   };
-  auto finalize_chunk = [&](XChunk& x) {
+  auto finalize_chunk = [&](XChunk& x) {   // FEDMX_HW_BIASX == 0
+    if (FEDMX_HW_BIASX) return;
 #pragma unroll
     for (int r = 0; r < 3; ++r)
       if (bias_col) x.b1[r] = 1.f;
@@ -505,6 +532,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         lds_write4(sK + 4 * (js & 1), f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f});
     };
     publish_k();   // step 0's
+    AdamStep KN = K;   // FEDMX_HW_KEARLY: the next step's scalars
     for (int ep = 0; ep < A.epochs; ++ep) {
       double acc_tr = 0.0;
       // W4 gradient + Adam between barrier #2 of step s and barrier #1 of s+1
@@ -513,6 +541,16 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         HSTAMP(hs, 0);
         __syncthreads();   // barrier #1 (main: layer-1 partials)
         HSTAMP(hs, 2);
+        if (FEDMX_HW_KEARLY) {
+          // step js+1's scalars into the other slot: the mains read slot js&1
+          // now and slot (js+1)&1 after barrier #1 of step js+1
+          const AdamStep Kcur = K;
+          next_constants();
+          KN = K;
+          K = Kcur;
+          if (lane == 0 && w8 == 4)
+            lds_write4(sK + 4 * ((js + 1) & 1), f32x4{KN.neg_step_size, KN.inv_bc2s, KN.bc2s, 0.f});
+        }
         __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
         HSTAMP(hs, 7);
         const f32x4 w4a0 = lds_read4(sT0 + tr);
@@ -545,7 +583,10 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         w4_to_lds(P4, L);
         publish_q4();
         ++js;
-        publish_k();   // step js's scalars, read by the mains after its barrier #1
+        if (FEDMX_HW_KEARLY)
+          K = KN;
+        else
+          publish_k();   // step js's scalars, read by the mains after its barrier #1
         HSTAMP(hs, 11);
       }
       double prox_now = 0.0;
@@ -786,6 +827,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       __syncthreads();  // barrier #2: dH3 partials of all waves visible
       HSTAMP(ms, 7);
       f32x4 dh3[2];
+#if FEDMX_HW_REDUCE == 0
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         f32x4 s = lds_read4(sRedDH3 + t * 256 + lane * 4);
@@ -799,6 +841,29 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         for (int r = 0; r < 4; ++r) s[r] = (hreal_d[t][r] && h3[t][r] > 0.f) ? s[r] : 0.f;
         dh3[t] = s;
       }
+#else
+      {
+        // all eight partial reads in flight before the first add (one LDS
+        // round trip; the compiler otherwise serialised them into six)
+        f32x4 pr[2][4];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int ww = 0; ww < 4; ++ww) pr[t][ww] = lds_read4(sRedDH3 + (ww * 2 + t) * 256 + lane * 4);
+        if (FEDMX_HW_REDUCE == 2) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          f32x4 s = pr[t][0];
+#pragma unroll
+          for (int ww = 1; ww < 4; ++ww)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[r] = s[r] + pr[t][ww][r];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[r] = (hreal_d[t][r] && h3[t][r] > 0.f) ? s[r] : 0.f;
+          dh3[t] = s;
+        }
+      }
+#endif
       float prox_acc = 0.f;
       ++step;
 #pragma unroll

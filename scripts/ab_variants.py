@@ -17,6 +17,14 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from fedmse_decentralized_amd.ops import build  # noqa: E402
 
 VARIANTS = {
+    # r3: helper-wave kernel step-loop fixes (scripts/gpu_train_ab.sh)
+    "r0b0": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0"],   # round-2 code paths
+    "r2b0": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0"],   # fenced dH3 reads only
+    "r0b1": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=0"],   # bias-column address select only
+    "r1b1": ["-DFEDMX_HW_REDUCE=1", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=0"],   # unfenced grouped reads + select
+    "r2b1": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=0"],   # both
+    "r0b0k": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=1"],  # early Adam scalars only
+    "r2b1k": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=1"],  # all three
     "base": [],                                   # defaults: compact order, FMA Adam, iglp_opt(0), VGPR-form MFMA
     "sched0": ["-DFEDMX_SCHED_HINTS=0"],          # compiler schedule          (+2.5%, measured)
     "hint1": ["-DFEDMX_SCHED_HINTS=1"],           # 64 x (1 MFMA, 6 VALU)      (+9%)

@@ -29,6 +29,8 @@ PAPER_IID = {  # mean AUC %, results_visualization.ipynb:33-50
     ("autoencoder", "avg"): 99.07, ("autoencoder", "fedprox"): 98.95, ("autoencoder", "mse_avg"): 98.92,
     ("hybrid", "avg"): 98.76, ("hybrid", "fedprox"): 98.53, ("hybrid", "mse_avg"): 99.01,
 }
+# SAE-CEN + MSEAvg against the client ratio, IID (results_visualization.ipynb:325-346)
+PAPER_RATIO_IID = {0.5: 99.01, 0.6: 98.96, 0.7: 98.44, 0.8: 98.71, 0.9: 98.60, 1.0: 98.69}
 
 
 def main():
@@ -39,6 +41,8 @@ def main():
     p.add_argument("--rounds", type=int, default=20)
     p.add_argument("--epochs", type=int, default=100)
     p.add_argument("--combos", default="all", help="e.g. hybrid:mse_avg,autoencoder:avg")
+    p.add_argument("--participation", type=float, nargs="+", default=[0.5],
+                   help="client ratio sweep (paper table: 0.5 .. 1.0)")
     args = p.parse_args()
 
     import torch
@@ -60,8 +64,9 @@ def main():
         json.dump(cfg_json, f)
     device = "cuda" if torch.cuda.is_available() and args.backend != "torch" else "cpu"
     combos = list(PAPER_IID) if args.combos == "all" else [tuple(c.split(":")) for c in args.combos.split(",")]
-    for model_type, update_type in combos:
-        cfg = ExperimentConfig(config_file=cfg_path, network_size=len(clients), num_participants=0.5,
+    todo = [(mt, ut, part) for mt, ut in combos for part in args.participation]
+    for model_type, update_type, part in todo:
+        cfg = ExperimentConfig(config_file=cfg_path, network_size=len(clients), num_participants=part,
                                epoch=args.epochs, num_rounds=args.rounds, lr_rate=1e-5, shrink_lambda=10,
                                model_types=[model_type], update_types=[update_type], backend=args.backend,
                                device=device, compat=args.compat, global_early_stop=False,
@@ -74,10 +79,14 @@ def main():
         dt = time.perf_counter() - t0
         m = np.asarray(fed.last_metrics, dtype=np.float64)
         print(json.dumps({
-            "model": model_type, "update": update_type, "backend": fed.engine.name, "compat": args.compat,
+            "model": model_type, "update": update_type, "participation": part, "backend": fed.engine.name,
+            "compat": args.compat,
             "rounds": fed.round_idx, "final_auc_mean_pct": round(100 * float(m.mean()), 3),
             "final_auc_std_pct": round(100 * float(m.std()), 3), "final_auc_min_pct": round(100 * float(m.min()), 3),
-            "best_auc_pct": round(100 * best, 3), "paper_iid_mean_pct": PAPER_IID.get((model_type, update_type)),
+            "best_auc_pct": round(100 * best, 3),
+            "paper_iid_mean_pct": (PAPER_IID.get((model_type, update_type)) if part == 0.5 else
+                                   PAPER_RATIO_IID.get(part) if (model_type, update_type) == ("hybrid", "mse_avg")
+                                   else None),
             "wall_s": round(dt, 2)}), flush=True)
 
 
