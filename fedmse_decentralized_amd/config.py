@@ -106,6 +106,14 @@ class ExperimentConfig:
     # as a single-rank federation on that rank's GPU) instead of every
     # combination being sharded over all ranks.
     parallel_combos: bool = False
+    # one process, one GPU: build every combination's federation up front and
+    # run their rounds interleaved, each federation on its own HIP stream and
+    # launch rings (ops/_hip.Runtime(private=True)), so their kernels overlap
+    # on the GPU's idle CUs and one federation's host work overlaps another's
+    # GPU work.  compat=fixed only (the reference's global early-stop state is
+    # shared across combinations in sequence); reports and the
+    # summary are identical to the sequential sweep.
+    concurrent_combos: bool = False
     # fixed compat + HIP engine: run the round's protocol decisions on the
     # device (engine/device_round.py) so rounds need no host synchronisation
     device_protocol: bool = True

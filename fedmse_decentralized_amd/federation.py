@@ -151,6 +151,8 @@ class Federation:
         self.last_metrics: Optional[np.ndarray] = None
         self.latent_log: Dict[int, Dict[str, Tuple[np.ndarray, np.ndarray]]] = {}
         self.writer = writer or _default_writer()
+        self.defer_verification = False     # set by the concurrent sweep (main.py)
+        self._deferred_vr: List[Tuple[int, List[Dict]]] = []
 
     # -- setup -------------------------------------------------------------------
     def setup(self):
@@ -250,7 +252,18 @@ class Federation:
                                     files=self.writer.files)
 
     def _report_verification(self, rnd: int, vr: List[Dict]) -> None:
+        if self.defer_verification:
+            # the run's verification file is shared by every combination
+            # (src/main.py:313-326): concurrent combinations hold their lines
+            # back and write them at conclude(), in combination order
+            self._deferred_vr.append((rnd, vr))
+            return
         reports.append_verification(self.cfg, self.run, rnd, vr, files=self.writer.files)
+
+    def _flush_deferred_verification(self) -> None:
+        for rnd, vr in self._deferred_vr:
+            reports.append_verification(self.cfg, self.run, rnd, vr, files=self.writer.files)
+        self._deferred_vr = []
 
     def _submit_checkpoints(self, res, local_sel: Sequence[int], snap, ev) -> None:
         # one job per round: every trained client's model.cpt + tracking pickle
@@ -570,14 +583,31 @@ class Federation:
         """Run ``num_rounds`` rounds (or until global early stop); returns the
         combination's best metric (max over clients of the final models,
         `src/main.py:367-374`)."""
+        while not self.step():
+            pass
+        return self.conclude()
+
+    def step(self) -> bool:
+        """One round of ``run_all`` (with its snapshot); True when the
+        combination is done (round limit reached or global early stop)."""
         cfg = self.cfg
-        while self.round_idx < cfg.num_rounds:
-            r = self.run_round()
-            if cfg.snapshot_every and self.round_idx % cfg.snapshot_every == 0:
-                self.save_snapshot()
-            if cfg.global_early_stop and r.stop:
-                break
+        if self.round_idx >= cfg.num_rounds:
+            return True
+        r = self.run_round()
+        if cfg.snapshot_every and self.round_idx % cfg.snapshot_every == 0:
+            self.save_snapshot()
+        if cfg.global_early_stop and r.stop:
+            return True
+        return self.round_idx >= cfg.num_rounds
+
+    def conclude(self) -> float:
+        """End of the combination: collect every round, flush the artefacts,
+        latent pickles; the combination's best metric."""
+        cfg = self.cfg
         self.finish()
+        if self.defer_verification and self.write_reports:
+            # after every round's report job (the writer runs jobs in order)
+            self.writer.submit(self._flush_deferred_verification)
         if self.last_metrics is None:
             er = self.engine.evaluate(self.model_type, cfg.metric)
             vec = torch.zeros(self.N, dtype=torch.float64)

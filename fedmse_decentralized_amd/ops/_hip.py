@@ -179,10 +179,23 @@ def _check(rc: int, what: str):
 
 
 class Runtime:
-    """Per-device launch context: the stream plus the mapped descriptor / result rings."""
+    """Per-device launch context: the stream plus the mapped descriptor / result rings.
 
-    def __init__(self, device: torch.device):
+    ``Runtime(device)`` is the process's default context (``runtime()``);
+    ``Runtime(device, private=True)`` is an independent one with its own
+    non-blocking stream and rings, made current with ``use_runtime`` — e.g.
+    one per federation when several run concurrently on one GPU
+    (``main.py --concurrent-combos``)."""
+
+    def __init__(self, device: torch.device, private: bool = False):
         self.device = device
+        if private:
+            s = torch.cuda.Stream(device=device)
+            self.torch_stream = s
+            self.stream = s.cuda_stream
+            self.desc = _hiprt.DescRing(1 << 20, self.stream)
+            self.out = _hiprt.OutRing(1 << 20, self.stream)
+            return
         cur = torch.cuda.current_stream(device)
         self.torch_stream = None
         if cur.cuda_stream == 0 and os.environ.get("FEDMX_NULL_STREAM", "0") != "1":
@@ -213,6 +226,9 @@ _tls = threading.local()
 
 
 def runtime(device: torch.device) -> Runtime:
+    ov = getattr(_tls, "rt_override", None)
+    if ov is not None and (device.index is None or device.index == ov.device.index):
+        return ov
     key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
     r = _runtimes.get(key)
     if r is None:
@@ -230,6 +246,29 @@ def runtime(device: torch.device) -> Runtime:
 def _stream(device: torch.device) -> int:
     s = getattr(_tls, "stream", None)
     return s if s is not None else runtime(device).stream
+
+
+class use_runtime:
+    """Make a private ``Runtime`` current for this thread: every launch, ring
+    descriptor and torch op inside the block goes to its stream.  ``None``
+    is a no-op (CPU engines)."""
+
+    def __init__(self, rt: Optional[Runtime]):
+        self.rt = rt
+        self._ctx = torch.cuda.stream(rt.torch_stream) if rt is not None else None
+
+    def __enter__(self):
+        if self.rt is not None:
+            self._prev = getattr(_tls, "rt_override", None)
+            _tls.rt_override = self.rt
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.rt is not None:
+            self._ctx.__exit__(*exc)
+            _tls.rt_override = self._prev
+        return False
 
 
 class on_stream:

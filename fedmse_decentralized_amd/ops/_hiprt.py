@@ -78,7 +78,7 @@ def stream_sync(stream: int) -> None:
     rc = rt().hipStreamSynchronize(ctypes.c_void_p(stream))
     if rc != 0:
         raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
-    SyncClock.tick()
+    SyncClock.tick(stream)
 
 
 def device_sync() -> None:
@@ -89,13 +89,24 @@ def device_sync() -> None:
 
 
 class SyncClock:
-    """Counts completed stream synchronisations (ring-reuse generations)."""
+    """Counts completed synchronisations (ring-reuse generations): a stream
+    synchronisation covers the rings of that stream only, a device
+    synchronisation every ring (several runtimes may share the process)."""
 
-    gen = 0
+    gen = 0                      # device-wide synchronisations
+    _stream_gen: dict = {}       # stream -> synchronisations of that stream
 
     @classmethod
-    def tick(cls):
-        cls.gen += 1
+    def tick(cls, stream: Optional[int] = None):
+        if stream is None:
+            cls.gen += 1
+        else:
+            cls._stream_gen[stream] = cls._stream_gen.get(stream, 0) + 1
+
+    @classmethod
+    def of(cls, stream: int) -> int:
+        """Monotone count of the synchronisations that cover ``stream``."""
+        return cls.gen + cls._stream_gen.get(stream, 0)
 
 
 class MappedBuffer:
@@ -223,14 +234,14 @@ class _Ring:
             self._retired.append(self.buf)
             self.buf = self.buffer_type(2 * nbytes)
             self.off = 0
-            self.wrap_gen = SyncClock.gen
+            self.wrap_gen = SyncClock.of(self.stream)
         if self.off + nbytes > self.buf.nbytes:
             # wrapping: earlier regions may still be read/written by queued kernels
             # unless a stream synchronisation happened since this pass began
-            if SyncClock.gen <= self.wrap_gen:
+            if SyncClock.of(self.stream) <= self.wrap_gen:
                 device_sync()   # kernels on any stream may still read the ring
             self.off = 0
-            self.wrap_gen = SyncClock.gen
+            self.wrap_gen = SyncClock.of(self.stream)
         o = self.off
         self.off += nbytes
         return o

@@ -37,18 +37,26 @@
 // into six LDS round trips), 1 = all eight reads first, 2 = same + a
 // scheduling fence after the reads
 #ifndef FEDMX_HW_REDUCE
-#define FEDMX_HW_REDUCE 2
+#define FEDMX_HW_REDUCE 0
 #endif
 // 1: the helpers form step s+1's Adam scalars (an f64 dependency chain) in
 // their idle window between barriers #1 and #2 of step s instead of right
 // before barrier #1, where they sat on the helpers' path
 #ifndef FEDMX_HW_KEARLY
-#define FEDMX_HW_KEARLY 1
+#define FEDMX_HW_KEARLY 0
+#endif
+// 1: software-pipelined step tail (no FedProx): dW1 tiles in the order the
+// next chunk's layer 1 consumes them, each tile's Adam overlapping the next
+// tiles' MFMAs, the first layer-1 half overlapping the last tiles' Adam;
+// stages separated by scheduling fences.  Same per-element arithmetic and
+// summation order as the plain tail (bit-identical parameters).
+#ifndef FEDMX_HW_PIPE
+#define FEDMX_HW_PIPE 0
 #endif
 // bias column of X: 1 = the bias lanes load from kBiasX (address select),
 // 0 = overwrite the loaded registers (finalize)
 #ifndef FEDMX_HW_BIASX
-#define FEDMX_HW_BIASX 1
+#define FEDMX_HW_BIASX 0
 #endif
 // issue priority of the main waves over their helpers (s_setprio level; 0: equal)
 #ifndef FEDMX_HW_PRIO
@@ -892,6 +900,58 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         dh1b[t] = acc;
       }
       HSTAMP(ms, 8);
+#if FEDMX_HW_PIPE   // 1: fenced stages, 2: source order only
+      if (!PROX) {
+        // ---- stage A: the two dW1 tiles the next layer-1 f0 half waits for
+#pragma unroll
+        for (int s = 0; s < KB; ++s) {
+          G1[0][0] = mfma16(cur.b0[s], dh1b[0][s], G1[0][0]);
+          G1[1][0] = mfma16(cur.b0[s], dh1b[1][s], G1[1][0]);
+        }
+        wave_sync();
+        if (FEDMX_HW_PIPE == 1) __builtin_amdgcn_sched_barrier(0);
+        // ---- stage B: the other two tiles + the small tile || Adam of (0,0), (1,0)
+        const f32x4 sa = lds_read4(w < 2 ? sT2 + tr + 16 * w * S_T : sDZT + tr);
+        const f32x4 sbz = lds_read4(sZT + tr);
+        const f32x4 sb = (w < 2) ? sbz : ((w == 2) ? h1b[0] : h1b[1]);
+#pragma unroll
+        for (int s = 0; s < KB; ++s) {
+          G1[0][1] = mfma16(cur.b1[s], dh1b[0][s], G1[0][1]);
+          G1[1][1] = mfma16(cur.b1[s], dh1b[1][s], G1[1][1]);
+        }
+#pragma unroll
+        for (int s = 0; s < KB; ++s) Go = mfma16(sa[s], sb[s], Go);
+        float pacc = 0.f;
+        adam4<false>(P.q1[0][0], M.q1[0][0], V.q1[0][0], AN.q1[0][0], G1[0][0], K, pacc);
+        adam4<false>(P.q1[1][0], M.q1[1][0], V.q1[1][0], AN.q1[1][0], G1[1][0], K, pacc);
+        HSTAMP(ms, 9);
+        if (FEDMX_HW_PIPE == 1) __builtin_amdgcn_sched_barrier(0);
+        // ---- stage C: next layer-1 f0 half || Adam of (0,1), (1,1)
+        f32x4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc0 = mfma16(P.q1[0][0][j], nxt.f0[j], acc0);
+          acc1 = mfma16(P.q1[1][0][j], nxt.f0[j], acc1);
+        }
+        adam4<false>(P.q1[0][1], M.q1[0][1], V.q1[0][1], AN.q1[0][1], G1[0][1], K, pacc);
+        adam4<false>(P.q1[1][1], M.q1[1][1], V.q1[1][1], AN.q1[1][1], G1[1][1], K, pacc);
+        HSTAMP(ms, 10);
+        if (FEDMX_HW_PIPE == 1) __builtin_amdgcn_sched_barrier(0);
+        // ---- stage D: next layer-1 f1 half || small-tile Adam, publish
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc0 = mfma16(P.q1[0][1][j], nxt.f1[j], acc0);
+          acc1 = mfma16(P.q1[1][1][j], nxt.f1[j], acc1);
+        }
+        l1a = acc0;
+        l1b = acc1;
+        adam4<false>(P.o, M.o, V.o, AN.o, Go, K, pacc);
+        own_to_lds(P, L);   // read by every wave after barrier #1
+        HSTAMP(ms, 11);
+        cur = nxt;
+        continue;
+      }
+#endif
       // ---- dW1^T (own columns) = X^T dH1
 #pragma unroll
       for (int s = 0; s < KB; ++s) {

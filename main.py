@@ -67,6 +67,12 @@ def run_sweep(cfg: ExperimentConfig, comm=None) -> dict:
     combos = [(mt, ut, run) for mt in cfg.model_types for ut in cfg.update_types for run in range(cfg.num_runs)]
     parallel = cfg.parallel_combos and comm.world_size > 1
     results = []
+    if cfg.concurrent_combos and not parallel:
+        if cfg.compat != "fixed":
+            raise SystemExit("--concurrent-combos needs --compat fixed (the reference's early-stop state is "
+                             "shared across combinations run in sequence)")
+        results = _run_concurrent(cfg, combos, comm, log)
+        combos = []
     for k, (model_type, update_type, run) in enumerate(combos, start=1):
         if parallel and (k - 1) % comm.world_size != comm.rank:
             continue
@@ -97,6 +103,41 @@ def run_sweep(cfg: ExperimentConfig, comm=None) -> dict:
     if own_comm:
         shutdown(comm)
     return best
+
+
+def _run_concurrent(cfg: ExperimentConfig, combos, comm, log):
+    """Every combination's federation at once on this process's device: each
+    gets its own HIP stream and launch rings, and their rounds are issued
+    round-robin, so the GPU runs several federations' kernels side by side
+    (a 10-client round occupies 5 of 256 CUs) while the host prepares the
+    next federation's round.  Per-combination results equal the sequential
+    sweep's (independent RNG streams, separate report files)."""
+    from fedmse_decentralized_amd.ops import _hip
+
+    cuda = comm.device.type == "cuda"
+    feds = []
+    for k, (model_type, update_type, run) in enumerate(combos, start=1):
+        log.info(f"\nStarting combination {k}/{len(combos)} (concurrent)")
+        log.info(f"Model type: {model_type}, Update type: {update_type}, Run: {run + 1}/{cfg.num_runs}")
+        rt = _hip.Runtime(comm.device, private=True) if cuda and cfg.backend != "torch" else None
+        with _hip.use_runtime(rt):
+            fed = Federation(cfg, model_type, update_type, run, comm=comm,
+                             early_stop=GlobalEarlyStop(cfg.global_patience, cfg.compat))
+            fed.defer_verification = True   # the run's verification file is shared: combination order
+            fed.setup()
+        feds.append((model_type, update_type, fed, rt))
+    active = list(range(len(feds)))
+    while active:
+        for i in list(active):
+            _, _, fed, rt = feds[i]
+            with _hip.use_runtime(rt):
+                if fed.step():
+                    active.remove(i)
+    results = []
+    for model_type, update_type, fed, rt in feds:
+        with _hip.use_runtime(rt):
+            results.append((model_type, update_type, fed.conclude()))
+    return results
 
 
 def main(argv=None):

@@ -18,13 +18,17 @@ from fedmse_decentralized_amd.ops import build  # noqa: E402
 
 VARIANTS = {
     # r3: helper-wave kernel step-loop fixes (scripts/gpu_train_ab.sh)
-    "r0b0": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0"],   # round-2 code paths
-    "r2b0": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0"],   # fenced dH3 reads only
-    "r0b1": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=0"],   # bias-column address select only
-    "r1b1": ["-DFEDMX_HW_REDUCE=1", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=0"],   # unfenced grouped reads + select
-    "r2b1": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=0"],   # both
-    "r0b0k": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=1"],  # early Adam scalars only
-    "r2b1k": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=1"],  # all three
+    "r0b0": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],   # round-2 code paths
+    "r2b0": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],   # fenced dH3 reads only
+    "r0b1": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],   # bias-column address select only
+    "r1b1": ["-DFEDMX_HW_REDUCE=1", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],   # unfenced grouped reads + select
+    "r2b1": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],   # both
+    "r0b0k": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=1", "-DFEDMX_HW_PIPE=0"],  # early Adam scalars only
+    "r2b1k": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=1", "-DFEDMX_HW_PIPE=0"],  # three
+    "r0b0p": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=1"],  # pipelined tail only
+    "r1b0": ["-DFEDMX_HW_REDUCE=1", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],  # grouped reads, unfenced
+    "r0b0q": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=2"],  # tail in pipeline order, unfenced
+    "r2b1kp": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=1", "-DFEDMX_HW_PIPE=1"],  # all four
     "base": [],                                   # defaults: compact order, FMA Adam, iglp_opt(0), VGPR-form MFMA
     "sched0": ["-DFEDMX_SCHED_HINTS=0"],          # compiler schedule          (+2.5%, measured)
     "hint1": ["-DFEDMX_SCHED_HINTS=1"],           # 64 x (1 MFMA, 6 VALU)      (+9%)

@@ -8,15 +8,24 @@ cd "$ROOT"
 OUT=$ROOT/gpurun_out/sweep
 mkdir -p "$OUT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-for compat in fixed reference fixed; do
+run_main() {  # label extra-args...
+  local label=$1; shift
   d=$(mktemp -d)
   s=$(date +%s.%N)
-  timeout -k 10 300 python main.py --synthetic nbaiot --compat $compat --output-root "$d" --log-level WARNING \
-    > "$OUT/main_$compat.log" 2>&1 || { echo "main $compat rc=$?"; tail -5 "$OUT/main_$compat.log"; exit 1; }
+  timeout -k 10 300 python main.py --synthetic nbaiot --output-root "$d" --log-level WARNING "$@" \
+    > "$OUT/main_$label.log" 2>&1 || { echo "main $label rc=$?"; tail -5 "$OUT/main_$label.log"; exit 1; }
   e=$(date +%s.%N)
-  echo "main.py --compat $compat wall_s=$(python -c "print(round($e-$s,3))") summary=$(tr -d '\n ' < "$d"/Checkpoint/Results/Update/10/*/training_summary.json)"
+  echo "main.py $* wall_s=$(python -c "print(round($e-$s,3))") summary_sha=$(sha256sum "$d"/Checkpoint/Results/Update/10/*/training_summary.json | cut -c1-16) reports_sha=$(find "$d"/Checkpoint/Results -name '*.json' | sort | xargs cat | sha256sum | cut -c1-16)"
   rm -rf "$d"
-done
+}
+run_main fixed --compat fixed
+run_main reference --compat reference
+run_main fixed_conc --compat fixed --concurrent-combos true
+run_main fixed2 --compat fixed
+run_main fixed_conc2 --compat fixed --concurrent-combos true
+# paper configuration sweep (100 epochs, 20 rounds, lr 1e-5, lambda 10): sequential vs concurrent
+run_main paper --compat fixed --epoch 100 --num-rounds 20 --lr-rate 1e-5 --shrink-lambda 10
+run_main paper_conc --compat fixed --epoch 100 --num-rounds 20 --lr-rate 1e-5 --shrink-lambda 10 --concurrent-combos true
 d=$(mktemp -d)
 timeout -k 10 300 python -m cProfile -o "$OUT/main_fixed.prof" main.py --synthetic nbaiot --compat fixed --output-root "$d" \
   --log-level WARNING > /dev/null 2>&1 || exit 1
