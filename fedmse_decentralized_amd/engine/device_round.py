@@ -232,6 +232,10 @@ class DeviceRound:
         # optional: HIP-event time of every round's training launch (bench.py
         # at N > 1 measures the wait for the slowest rank's largest client)
         self.train_timing = False
+        # global early stop reads each round's metrics: collect right after
+        # enqueueing (False: the caller reads them later, e.g. after issuing
+        # other federations' rounds -- main.py --concurrent-combos)
+        self.eager_collect = True
         self.train_ms: Dict[int, float] = {}
         self.all_rounds: Dict[int, dict] = {}
         self.host_agg_counts = [0] * N
@@ -566,7 +570,7 @@ class DeviceRound:
         while len(self.pending) > self.max_pending:
             with tel.phase("collect"):    # mostly waiting for round r-2 on the GPU
                 self._collect(self.pending.popleft())
-        if cfg.global_early_stop:
+        if cfg.global_early_stop and self.eager_collect:
             self.collect_until(rnd)
         return res
 

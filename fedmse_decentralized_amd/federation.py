@@ -590,10 +590,21 @@ class Federation:
     def step(self) -> bool:
         """One round of ``run_all`` (with its snapshot); True when the
         combination is done (round limit reached or global early stop)."""
+        return self.end_step(self.begin_step())
+
+    def begin_step(self):
+        """Issue the next round (on the device path: enqueue it, results
+        collected lazily); None when the round limit is reached."""
+        if self.round_idx >= self.cfg.num_rounds:
+            return None
+        return self.run_round()
+
+    def end_step(self, r) -> bool:
+        """Finish a round from ``begin_step``: snapshot, early-stop decision
+        (which reads the round's metrics); True when the combination is done."""
         cfg = self.cfg
-        if self.round_idx >= cfg.num_rounds:
+        if r is None:
             return True
-        r = self.run_round()
         if cfg.snapshot_every and self.round_idx % cfg.snapshot_every == 0:
             self.save_snapshot()
         if cfg.global_early_stop and r.stop:

@@ -204,6 +204,37 @@ __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4
 #endif
 }
 
+// adam4 (FMA form) on float pairs: every non-transcendental step is one
+// packed-fp32 instruction for two parameters (v_pk_add / v_pk_mul /
+// v_pk_fma_f32: the same per-element IEEE results as the scalar ops, so the
+// update is bit-identical to adam4).  No FedProx term (its loss sum keeps the
+// scalar order).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void adam4_packed(float (&p)[4], float (&m)[4], float (&v)[4], f32x4 g,
+                                             const AdamStep& K) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const f32x2 G = {g[2 * h], g[2 * h + 1]};
+    f32x2 M = {m[2 * h], m[2 * h + 1]};
+    f32x2 V = {v[2 * h], v[2 * h + 1]};
+    f32x2 P = {p[2 * h], p[2 * h + 1]};
+    const f32x2 omb1 = {K.one_m_b1, K.one_m_b1}, b2 = {K.b2, K.b2}, omb2 = {K.one_m_b2, K.one_m_b2};
+    const f32x2 ibc = {K.inv_bc2s, K.inv_bc2s}, eps = {K.eps, K.eps}, ns = {K.neg_step_size, K.neg_step_size};
+    M = __builtin_elementwise_fma(omb1, G - M, M);
+    V = __builtin_elementwise_fma(omb2 * G, G, V * b2);
+    f32x2 d = {__builtin_amdgcn_sqrtf(V.x), __builtin_amdgcn_sqrtf(V.y)};
+    d = __builtin_elementwise_fma(d, ibc, eps);
+    const f32x2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    P = __builtin_elementwise_fma(ns, M * r, P);
+    m[2 * h] = M.x;
+    m[2 * h + 1] = M.y;
+    v[2 * h] = V.x;
+    v[2 * h + 1] = V.y;
+    p[2 * h] = P.x;
+    p[2 * h + 1] = P.y;
+  }
+}
+
 // dense global [P_PAD] <-> LDS masters
 __device__ __forceinline__ void global_to_masters(const float* __restrict__ src, float* sW1, float* sW4,
                                                   float* sW2, float* sW3) {

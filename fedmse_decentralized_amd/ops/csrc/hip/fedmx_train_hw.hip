@@ -28,7 +28,10 @@
 
 // Timing-only ablations of the main waves' step (WRONG numerics, never a
 // production build): 2 = no loss accumulation, 4 = no small-tile gradient /
-// Adam.  (1 = no per-step Adam constants on the mains, -6.3 %, led to the
+// Adam, 8 = every prefetch reads the epoch's first chunk (cache-resident:
+// what the prefetch's memory latency costs), 16 = helpers skip W4's Adam
+// (G4 folded in with one FMA per parameter), 32 = mains skip W1's Adam
+// (same), 64 = helpers do nothing between the barriers.  (1 = no per-step Adam constants on the mains, -6.3 %, led to the
 // helper-side computation below.)
 #ifndef FEDMX_HW_ABLATE
 #define FEDMX_HW_ABLATE 0
@@ -52,6 +55,10 @@
 // summation order as the plain tail (bit-identical parameters).
 #ifndef FEDMX_HW_PIPE
 #define FEDMX_HW_PIPE 0
+#endif
+// 1: the Adam updates without FedProx in packed-fp32 form (adam4_packed)
+#ifndef FEDMX_HW_PACKED
+#define FEDMX_HW_PACKED 0
 #endif
 // bias column of X: 1 = the bias lanes load from kBiasX (address select),
 // 0 = overwrite the loaded registers (finalize)
@@ -561,6 +568,14 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         }
         __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
         HSTAMP(hs, 7);
+        if (FEDMX_HW_ABLATE & 64) {
+          ++js;
+          if (FEDMX_HW_KEARLY)
+            K = KN;
+          else
+            publish_k();
+          continue;
+        }
         const f32x4 w4a0 = lds_read4(sT0 + tr);
         const f32x4 w4a1 = lds_read4(sT0 + tr + 16 * S_T);
         const f32x4 w4b0 = lds_read4(sT1 + tr);
@@ -582,8 +597,16 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
         for (int v = 0; v < 2; ++v)
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
-            adam4<PROX>(P4.q4[v][t], M4.q4[v][t], V4.q4[v][t], AN4.q4[v][t], G4[v][t], K, prox_acc);
+          for (int t = 0; t < 2; ++t) {
+            if (FEDMX_HW_ABLATE & 16) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) P4.q4[v][t][r] = __builtin_fmaf(G4[v][t][r], 0.f, P4.q4[v][t][r]);
+            } else if (FEDMX_HW_PACKED && !PROX) {
+              adam4_packed(P4.q4[v][t], M4.q4[v][t], V4.q4[v][t], G4[v][t], K);
+            } else {
+              adam4<PROX>(P4.q4[v][t], M4.q4[v][t], V4.q4[v][t], AN4.q4[v][t], G4[v][t], K, prox_acc);
+            }
+          }
         if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
         HSTAMP(hs, 10);
         // publish W4(s+1): master rows (layer 4, validation, snapshots) and the
@@ -788,7 +811,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         if (!(FEDMX_HW_ABLATE & 2)) acc_tr += (double)contrib;
         HSTAMP(ms, 3);
       }
-      if (has_next) load_chunk(Xtr, row_n, bc_n, nxt);  // prefetch
+      if (has_next) load_chunk(Xtr, (FEDMX_HW_ABLATE & 8) ? 0 : row_n, bc_n, nxt);  // prefetch (ablation 8: chunk 0, cached)
 
       float q2[2][4], q3[2][4];
 #pragma unroll
@@ -974,12 +997,26 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int v = 0; v < 2; ++v) adam4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
+        for (int v = 0; v < 2; ++v) {
+          if (FEDMX_HW_ABLATE & 32) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) P.q1[t][v][r] = __builtin_fmaf(G1[t][v][r], 0.f, P.q1[t][v][r]);
+          } else if (FEDMX_HW_PACKED && !PROX) {
+            adam4_packed(P.q1[t][v], M.q1[t][v], V.q1[t][v], G1[t][v], K);
+          } else {
+            adam4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
+          }
+        }
       HSTAMP(ms, 10);
       // (after an epoch's last batch this works on a stale tile; unused)
       finalize_chunk(nxt);
       l1_partial(nxt, l1a, l1b);
-      if (!(FEDMX_HW_ABLATE & 4)) adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
+      if (!(FEDMX_HW_ABLATE & 4)) {
+        if (FEDMX_HW_PACKED && !PROX)
+          adam4_packed(P.o, M.o, V.o, Go, K);
+        else
+          adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
+      }
       if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
       if (!(FEDMX_HW_ABLATE & 4)) own_to_lds(P, L);   // read by every wave after barrier #1
       HSTAMP(ms, 11);

@@ -126,12 +126,20 @@ def _run_concurrent(cfg: ExperimentConfig, combos, comm, log):
             fed.defer_verification = True   # the run's verification file is shared: combination order
             fed.setup()
         feds.append((model_type, update_type, fed, rt))
+    for _, _, fed, _ in feds:
+        if getattr(fed, "_fast", None) is not None:
+            fed._fast.eager_collect = False   # issue every federation's round before reading any
     active = list(range(len(feds)))
     while active:
-        for i in list(active):
+        issued = []
+        for i in active:
             _, _, fed, rt = feds[i]
             with _hip.use_runtime(rt):
-                if fed.step():
+                issued.append((i, fed.begin_step()))
+        for i, r in issued:
+            _, _, fed, rt = feds[i]
+            with _hip.use_runtime(rt):
+                if fed.end_step(r):
                     active.remove(i)
     results = []
     for model_type, update_type, fed, rt in feds:

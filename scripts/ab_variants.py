@@ -28,6 +28,11 @@ VARIANTS = {
     "r0b0p": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=1"],  # pipelined tail only
     "r1b0": ["-DFEDMX_HW_REDUCE=1", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],  # grouped reads, unfenced
     "r0b0q": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=2"],  # tail in pipeline order, unfenced
+    "packed": ["-DFEDMX_HW_PACKED=1"],               # packed-fp32 Adam (bit-identical)
+    "abl_pf": ["-DFEDMX_HW_ABLATE=8"],               # timing only: prefetch always hits the cache
+    "abl_hadam": ["-DFEDMX_HW_ABLATE=16"],           # timing only: helpers skip W4's Adam
+    "abl_madam": ["-DFEDMX_HW_ABLATE=32"],           # timing only: mains skip W1's Adam
+    "abl_hnone": ["-DFEDMX_HW_ABLATE=64"],           # timing only: helpers idle between barriers
     "r2b1kp": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=1", "-DFEDMX_HW_PIPE=1"],  # all four
     "base": [],                                   # defaults: compact order, FMA Adam, iglp_opt(0), VGPR-form MFMA
     "sched0": ["-DFEDMX_SCHED_HINTS=0"],          # compiler schedule          (+2.5%, measured)
