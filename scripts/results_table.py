@@ -1,6 +1,6 @@
-"""Results tables from the per-round report files (the role of the reference's
-`src/Visualization/results_visualization.ipynb`, SURVEY C36, without
-matplotlib, which this image does not ship).
+"""Results tables from the per-round report files (the tabular half of the
+reference's `src/Visualization/results_visualization.ipynb`; the
+figures are `scripts/plots.py`).
 
 Reads every ``*_results.json`` (one JSON line per round:
 ``{round, client_metrics, update_type, model_type, global_loss}``) under a

@@ -141,3 +141,36 @@ def test_bench_gpus_flag_spawns_ranks_without_a_launcher():
     assert s10["federation_rounds_per_sec"] > 0 and 0.0 <= s10["detection_auc_mean"] <= 1.0
     # non-overlapping phase telemetry: the phases sum to at most the timed region
     assert sum(rec["phase_ms_total"].values()) <= rec["timed_ms"] * 1.001
+
+
+def test_plots_scale_combos_and_tsne(tmp_path):
+    """scripts/plots.py (the reference notebooks' figures): AUC-vs-size bars
+    from network_scale records, per-combination bars from report files, and
+    a latent t-SNE from a --save-latents pickle of a tiny CPU run."""
+    import dataclasses
+
+    import plots
+    from fedmse_decentralized_amd.config import ExperimentConfig
+    from fedmse_decentralized_amd.federation import Federation
+
+    recs = tmp_path / "s.jsonl"
+    with open(recs, "w") as f:
+        for n, a in ((10, 0.985), (20, 0.986)):
+            f.write(json.dumps({"clients": n, "participation": 0.5, "iid": True, "rounds": 50, "backend": "hip",
+                                "init_mode": "shared", "auc_mean_last10": a}) + "\n")
+    assert os.path.getsize(plots.plot_sweep([str(recs)], "clients", plots.SCALE_REF, "clients",
+                                            str(tmp_path / "scale.png"), "t")) > 1000
+    cfg = ExperimentConfig(synthetic="nbaiot", network_size=3, num_rounds=2, epoch=1, output_root=str(tmp_path),
+                           backend="torch", device="cpu", compat="fixed", save_checkpoints=False, save_latents=True,
+                           global_early_stop=False, log_level="WARNING", model_types=["hybrid"],
+                           update_types=["mse_avg"])
+    from test_distributed import _shrink
+
+    _shrink()
+    fed = Federation(dataclasses.replace(cfg), "hybrid", "mse_avg", 0).setup()
+    fed.run_all()
+    run_dir = os.path.join(str(tmp_path), "Checkpoint/LatentData/3", cfg.experiment_name, "Run_0")
+    out = plots.plot_tsne(run_dir, fed.clients[0].name, str(tmp_path / "tsne.png"))
+    assert os.path.getsize(out) > 1000
+    out = plots.plot_combos(os.path.join(str(tmp_path), "Checkpoint/Results"), str(tmp_path / "combos.png"))
+    assert os.path.getsize(out) > 1000
