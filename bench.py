@@ -52,10 +52,13 @@ EPISODE = 20   # paper schedule: 20 rounds per run; aggregation caps reset per e
 def _collectives_label(comm) -> str:
     """What carries the per-round exchange: RCCL (torch.distributed "nccl"
     on ROCm), gloo, or nothing (one rank: in-process loopback).  "xGMI" only
-    when the ranks sit on distinct GPUs (launch.collective_self_test)."""
+    when several ranks sit on distinct GPUs (launch.collective_self_test)."""
     if type(comm).__name__ == "PhantomComm":
         return "collectives stubbed: one-GPU projection of rank 0"
-    link = "over xGMI" if getattr(comm, "devices_distinct", False) else "ranks share one GPU"
+    if getattr(comm, "world_size", 1) <= 1:
+        link = "one rank"
+    else:
+        link = "over xGMI" if getattr(comm, "devices_distinct", False) else "ranks share one GPU"
     if getattr(comm, "active", False):
         return f"peer-memory one-shot all-gather/all-reduce (IPC, {link})"
     try:
