@@ -223,40 +223,6 @@ class DeviceRound:
         # 2 = sample-weighted FedAvg (host-computed: they depend on the selection only)
         self.rule = 1 if fed.update_type == "mse_avg" else (2 if cfg.fedavg_sample_weighted else 0)
         self.n_train = {c: fed.clients[c].train.shape[0] for c in range(N)}
-        # Early scoring: the vote / FedMSE forwards and their reduction run on
-        # a stream of their own while the round's training kernel is still
-        # going.  Each training workgroup bumps a started counter and, once
-        # its client's parameters are written, sets done[store row] = the
-        # round's sequence number; a one-wave start gate holds the forward
-        # back until every trainer is resident, then each forward block waits
-        # for its own model's flag (fwd_rows_kernel<true>).  The scores of all
-        # but the last-finishing clients are ready when training ends.
-        # Opt-in (FEDMX_EARLY_SCORE=1): measured slower at the benchmark's
-        # shape (profiles/r3_early_scoring.md); never with injected poisoning
-        # (applied after training on the main stream).
-        self.early = (bool(fed.local) and not cfg.malicious_clients
-                      and os.environ.get("FEDMX_EARLY_SCORE", "0") == "1")
-        if self.early:
-            self.score_stream = torch.cuda.Stream(device=dev)
-            self.started = torch.zeros(1, dtype=i32, device=dev)
-            self.done = torch.zeros(st.params.shape[0], dtype=i32, device=dev)
-            self.seq = 0
-            self.started_target = 0
-            # wait-timeout codes (1: a model's done flag, 2: the start gate),
-            # written by the device into mapped host memory
-            self.err_buf = _hip._hiprt.MappedBuffer(64)
-            self.err = self.err_buf.view(0, np.int32, 1)
-            self.err[:] = 0
-            vmax = max(int(v.shape[0]) for v in fed.valid_all)
-            ndev = int(fed.dev_set.shape[0]) if self.rule == 1 else 0
-            self.score_sse = torch.empty(max(self.n_local * (vmax + ndev), 1), dtype=f32, device=dev)
-            # a generous bound on one training launch (15x the measured ~3.3 us
-            # per step, plus 5 s): a timeout means a trainer never finished
-            hp = fed.hp
-            ntr = max(int(fed.clients[c].train.shape[0]) for c in fed.local)
-            steps = hp.epochs * (-(-ntr // max(hp.batch_size, 1)) + -(-vmax // 16))
-            self.wait_timeout_us = 5_000_000 + 50 * steps
-            _hip.realtime_ticks_per_us(dev)   # calibrate the wait clock now, not mid-round
         # protocol variants the kernels implement: majority election (every
         # selected client votes) and the centralised push (no verification)
         self.thesis = cfg.protocol_variant == "thesis"
@@ -399,15 +365,7 @@ class DeviceRound:
             if self.train_timing and local_sel:
                 tev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 tev[0].record()
-            signal = ev0 = None
-            if self.early and local_sel:
-                self.seq += 1
-                ev0 = torch.cuda.Event()
-                ev0.record()
-                signal = (self.started, self.done, self.seq)
-            handle = eng.train_launch(local_rows, fed.hp, signal=signal) if local_sel else None
-            if signal is not None:
-                self.started_target += len(local_rows)
+            handle = eng.train_launch(local_rows, fed.hp) if local_sel else None
             if tev is not None:
                 tev[1].record()
                 rec["train_ev"] = tev
@@ -417,7 +375,7 @@ class DeviceRound:
                     st.params[self._loc(c)].mul_(cfg.malicious_scale)
         with tel.phase("vote"):
             if local_sel:
-                if ev_std is not None and not self.early:
+                if ev_std is not None:
                     torch.cuda.current_stream(dev).wait_event(ev_std)
                 need_dev = self.rule == 1
                 items = [(r, vs) for r in local_rows]
@@ -435,28 +393,12 @@ class DeviceRound:
                     items += [(r, fed.dev_set) for r in local_rows]
                     outs += [p + 16 for p in recp]
                     batch += [0] * len(local_rows)
+                sse, _ = _hip.forward_rows(st.params, items, fed.dims, True, False)
                 # multi-rank: the exchange's pack (row 1 + j of the send buffer =
-                # the j-th local selection's parameters) rides the score reduction
+                # the j-th local selection's parameters) rides the same launch
                 copies = [(st.params[self._loc(c)].data_ptr(), self.xsend[1 + j].data_ptr(), P_PAD)
                           for j, c in enumerate(local_sel)] if comm.collective and not _PACK_SEPARATE else ()
-                if self.early:
-                    # after ev0 (the previous round's election has read vec /
-                    # the exchange buffer, and its reduction the SSE buffer)
-                    ss = self.score_stream
-                    ss.wait_event(ev0)
-                    if ev_std is not None:
-                        ss.wait_event(ev_std)
-                    with _hip.on_stream(ss):
-                        sse = _hip.forward_rows_wait(st.params, items, fed.dims, self.done, self.seq, self.started,
-                                                     self.started_target, self.err_buf.dev_ptr,
-                                                     self.wait_timeout_us, ss.cuda_stream, out=self.score_sse)
-                        _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs, copies)
-                    ev_sc = torch.cuda.Event()
-                    ev_sc.record(ss)
-                    torch.cuda.current_stream(dev).wait_event(ev_sc)
-                else:
-                    sse, _ = _hip.forward_rows(st.params, items, fed.dims, True, False)
-                    _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs, copies)
+                _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs, copies)
         with tel.phase("comm"):
             if not comm.collective:
                 base = st.params
@@ -645,10 +587,6 @@ class DeviceRound:
         fed = self.fed
         cfg, eng = fed.cfg, fed.engine
         rec["event"].synchronize()
-        if self.early and int(self.err[0]) != 0:
-            raise RuntimeError(f"early scoring: a wait timed out on the device (code {int(self.err[0])}: "
-                               "1 = a model's done flag, 2 = the trainers' start gate); "
-                               "FEDMX_EARLY_SCORE=0 scores after training instead")
         if hasattr(fed.comm, "check"):
             fed.comm.check()   # peer-memory exchange: no wait of this round timed out
         N = self.N

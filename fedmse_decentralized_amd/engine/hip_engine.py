@@ -61,8 +61,8 @@ class HipEngine(Engine):
         return out
 
     # -- training ------------------------------------------------------------------
-    def train_launch(self, local_ids: Sequence[int], hp: TrainHParams, signal=None) -> TrainHandle:
-        trk, er, be = _hip.train(self.store, list(local_ids), hp, self.dims, signal=signal)
+    def train_launch(self, local_ids: Sequence[int], hp: TrainHParams) -> TrainHandle:
+        trk, er, be = _hip.train(self.store, list(local_ids), hp, self.dims)
         return TrainHandle(list(local_ids), [trk, er, be])
 
     def train_collect(self, handle: TrainHandle, host: Optional[List[np.ndarray]] = None) -> TrainResult:

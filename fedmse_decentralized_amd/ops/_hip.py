@@ -45,7 +45,7 @@ _lib = None
 FWD_DTYPE = np.dtype([
     ("params", "<u8"), ("x", "<u8"), ("sse", "<u8"), ("lat", "<u8"),
     ("nrows", "<i4"), ("lat_stride", "<i4"), ("d_in", "<i4"), ("latent", "<i4"),
-    ("hidden", "<i4"), ("wait_seq", "<i4"), ("wait_flag", "<u8"),
+    ("hidden", "<i4"), ("pad0", "<i4"), ("pad1", "<i8"),
 ])
 CEN_DTYPE = np.dtype([
     ("train_lat", "<u8"), ("test_lat", "<u8"), ("out", "<u8"),
@@ -72,8 +72,6 @@ class TrainArgs(ctypes.Structure):
         ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
         ("eps", ctypes.c_float), ("lam", ctypes.c_float), ("mu", ctypes.c_float),
         ("stamps", ctypes.c_void_p), ("flags", ctypes.c_int32), ("pad0", ctypes.c_int32),
-        # early scoring signals (fedmx_train_common.h): started counter, done flags, round sequence
-        ("started", ctypes.c_void_p), ("done", ctypes.c_void_p), ("seq", ctypes.c_int32), ("pad1", ctypes.c_int32),
     ]
 
 
@@ -130,7 +128,6 @@ def lib():
             vp, i32 = ctypes.c_void_p, ctypes.c_int
             sig = {
                 "fedmx_forward_rows": [vp, i32, vp],
-                "fedmx_forward_rows_wait": [vp, i32, vp, ctypes.c_int32, vp, ctypes.c_int64, vp],
                 "fedmx_weighted_sum": [vp, vp, i32, i32, vp, vp],
                 "fedmx_param_drift": [vp, i32, vp, vp, vp, vp],
                 "fedmx_standardize_lds": [vp, i32, i32, vp, vp],
@@ -141,7 +138,6 @@ def lib():
                 "fedmx_broadcast_rows": [vp, vp, vp, i32, vp, i32, vp],
                 "fedmx_train": [ctypes.POINTER(TrainArgs), i32, vp],
                 "fedmx_probe_mfma": [vp, vp],
-                "fedmx_probe_realtime": [vp, vp],
                 "fedmx_elect_wsum": [ctypes.POINTER(ElectArgs), ctypes.POINTER(WsumArgs), vp],
                 "fedmx_decide_adopt": [ctypes.POINTER(DecideArgs), vp],
                 "fedmx_verify_decide": [ctypes.POINTER(VerifyArgs), vp],
@@ -456,69 +452,6 @@ def forward_rows(params: torch.Tensor, items, dims, want_sse=True, want_latent=F
     return sse_l, lat_l
 
 
-_RT_RATE: Dict[int, float] = {}
-
-
-def realtime_ticks_per_us(device: torch.device) -> float:
-    """Rate of the device's constant clock (s_memrealtime), measured once per
-    device against the host clock: two probe reads ~50 ms apart."""
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    r = _RT_RATE.get(idx)
-    if r is None:
-        import time
-
-        out = torch.zeros(2, dtype=torch.int64, device=device)
-        s = _stream(device)
-        _check(lib().fedmx_probe_realtime(out.data_ptr(), s), "fedmx_probe_realtime")
-        _hiprt.stream_sync(s)
-        t0 = time.perf_counter()
-        time.sleep(0.05)
-        _check(lib().fedmx_probe_realtime(out.data_ptr() + 8, s), "fedmx_probe_realtime")
-        _hiprt.stream_sync(s)
-        t1 = time.perf_counter()
-        a, b = out.tolist()
-        r = _RT_RATE[idx] = max((b - a) / ((t1 - t0) * 1e6), 1e-3)
-    return r
-
-
-def forward_rows_wait(params: torch.Tensor, items, dims, done: torch.Tensor, seq: int, started: torch.Tensor,
-                      target: int, err_ptr: int, timeout_us: int, stream: int, out: Optional[torch.Tensor] = None):
-    """``forward_rows`` (SSE only) for early scoring, on ``stream``: a start
-    gate (``target`` training workgroups have begun: every trainer resident),
-    then the forward, each block waiting until ``done[row] == seq`` for its
-    item's parameter row.  ``out``: preallocated SSE buffer (>= total rows),
-    else allocated on the caller's current stream.  Wait timeouts write a
-    nonzero code to ``err_ptr`` (mapped host memory)."""
-    dev = params.device
-    _check_rows(items, dev)
-    rt = runtime(dev)
-    sizes = np.array([int(x.shape[0]) for _, x in items], dtype=np.int64)
-    tot = int(sizes.sum())
-    if out is None:
-        out = torch.empty(tot, dtype=torch.float32, device=dev)
-    elif out.numel() < tot or out.dtype != torch.float32:
-        raise ValueError("forward_rows_wait: SSE buffer too small")
-    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
-    P = params.shape[1]
-    rows = np.array([int(r) for r, _ in items], dtype=np.int64)
-    pptr = params.data_ptr() + 4 * P * rows
-    xptr = np.array([x.data_ptr() for _, x in items], dtype=np.int64)
-    sptr = out.data_ptr() + 4 * offs
-    desc = build_fwd_desc(pptr, xptr, sizes, sptr, np.zeros(len(items), np.int64), dims)
-    if len(desc):
-        # the block's item: its parameter address identifies the row
-        row_of = dict(zip(pptr.tolist(), rows.tolist()))
-        live = desc["nrows"] > 0
-        brow = np.array([row_of.get(int(p), 0) for p in desc["params"]], dtype=np.int64)
-        desc["wait_seq"] = np.where(live, int(seq), 0)
-        desc["wait_flag"] = np.where(live, done.data_ptr() + 4 * brow, 0)
-        (dptr,) = rt.desc.put(desc)
-        ticks = max(int(timeout_us * realtime_ticks_per_us(dev)), 1)
-        _check(lib().fedmx_forward_rows_wait(dptr, len(desc), started.data_ptr(), int(target), err_ptr,
-                                             ticks, stream), "fedmx_forward_rows_wait")
-    return [out[o:o + n] for o, n in zip(offs, sizes)]
-
-
 class FwdPlan:
     """A cached forward launch over fixed (param row, buffer) items."""
 
@@ -644,7 +577,6 @@ def score_reduce_to(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in
     reductions (the multi-rank exchange's pack)."""
     dev = sse_list[0].device
     rt = runtime(dev)
-    stream = _stream(dev)   # on_stream routes it (early scoring)
     desc = np.zeros(len(sse_list), dtype=SEG_DTYPE)
     desc["sse"] = [s.data_ptr() for s in sse_list]
     desc["n"] = [int(s.shape[0]) for s in sse_list]
@@ -652,7 +584,7 @@ def score_reduce_to(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in
     desc["out"] = np.asarray(out_ptrs, dtype=np.int64)
     if not copies:
         (dptr,) = rt.desc.put(desc)
-        _check(lib().fedmx_score_reduce(dptr, len(desc), d_in, stream), "fedmx_score_reduce")
+        _check(lib().fedmx_score_reduce(dptr, len(desc), d_in, rt.stream), "fedmx_score_reduce")
         return
     cd = np.zeros(len(copies), dtype=COPY_DTYPE)
     cd["src"] = [c[0] for c in copies]
@@ -661,7 +593,7 @@ def score_reduce_to(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in
     if bool(np.any(cd["nfloats"] % 4)):
         raise ValueError("score_reduce_to: copies must move whole float4 words")
     dptr, cptr = rt.desc.put(desc, cd)
-    _check(lib().fedmx_score_reduce_copy(dptr, len(desc), d_in, cptr, len(cd), stream), "fedmx_score_reduce_copy")
+    _check(lib().fedmx_score_reduce_copy(dptr, len(desc), d_in, cptr, len(cd), rt.stream), "fedmx_score_reduce_copy")
 
 
 def seg_desc_device(sse_list: Sequence[torch.Tensor], batch: Sequence[int], out_ptrs: Sequence[int], dev) -> torch.Tensor:
@@ -763,12 +695,10 @@ class TrainBuffers:
 
 
 def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tensor] = None,
-          compact: Optional[bool] = None, helper: Optional[bool] = None, signal=None):
+          compact: Optional[bool] = None, helper: Optional[bool] = None):
     """Launch the fused training kernel for store rows ``local_ids`` (async).
     Returns host views (tracking[k, E, 2], epochs_run[k], best_epoch[k])
-    written by the kernel, valid after the next stream sync.  ``signal``:
-    (started counter, done flags [store rows], seq) device tensors / value
-    for early scoring (``forward_rows_wait``)."""
+    written by the kernel, valid after the next stream sync."""
     dev = store.params.device
     rt = runtime(dev)
     k = len(local_ids)
@@ -803,11 +733,6 @@ def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tens
     a.lam, a.mu = hp.shrink_lambda, hp.fedprox_mu
     a.stamps = stamps.data_ptr() if stamps is not None else None
     a.flags = 0 if (TRAIN_COMPACT if compact is None else compact) else TRAIN_FLAG_NO_COMPACT
-    if signal is not None:
-        started, done, seq = signal
-        if done.dtype != torch.int32 or done.numel() < store.params.shape[0] or started.dtype != torch.int32:
-            raise ValueError("train: signal needs int32 started[1] and done[store rows]")
-        a.started, a.done, a.seq = started.data_ptr(), done.data_ptr(), int(seq)
     helper_on = TRAIN_HELPER if helper is None else helper
     if helper_on is not None:
         a.flags |= TRAIN_FLAG_HELPER if helper_on else TRAIN_FLAG_NO_HELPER

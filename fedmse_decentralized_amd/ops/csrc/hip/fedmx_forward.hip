@@ -15,60 +15,7 @@
 
 namespace fedmx {
 
-// ---------------------------------------------------------------------------
-// Early scoring (engine/device_round.py): the vote / FedMSE forwards run on a
-// second stream while the round's training kernel is still going, each block
-// waiting for its own model's done flag (TrainArgs::done).  Spins are bounded
-// by a wall-clock limit (s_memrealtime): on expiry the block records
-// an error code in `err` (mapped host memory, checked by the host when it
-// collects the round) and carries on, so no wait can hang the device.
-// s_sleep(8) (~512 clocks) repeats between two polls of a done flag
-#ifndef FEDMX_POLL_SLEEPS
-#define FEDMX_POLL_SLEEPS 1
-#endif
-__device__ inline bool seq_before(int32_t have, int32_t want) { return (int32_t)((uint32_t)have - (uint32_t)want) < 0; }
-
-__device__ inline void record_error(int32_t* err, int32_t code) {
-  if (err != nullptr) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// thread 0 spins, then the whole block acquires (its later loads of the model
-// see the trainer's released stores)
-__device__ inline void block_wait_flag(const int32_t* flag, int32_t seq, int32_t* err, uint64_t timeout) {
-  if (threadIdx.x == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (seq_before(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), seq)) {
-      for (int i = 0; i < FEDMX_POLL_SLEEPS; ++i) __builtin_amdgcn_s_sleep(8);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-        record_error(err, 1);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-
-// One wave: returns once `target` training workgroups have started (the
-// counter TrainArgs::started), i.e. every trainer of the round is resident.
-// Launched on the scoring stream right before the waiting forward: until it
-// returns, none of the forward's blocks occupies a CU a trainer still needs.
-__global__ __launch_bounds__(64) void start_gate_kernel(const int32_t* started, int32_t target, int32_t* err,
-                                                        uint64_t timeout) {
-  if (threadIdx.x != 0) return;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (seq_before(__hip_atomic_load(started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), target)) {
-    __builtin_amdgcn_s_sleep(8);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-      record_error(err, 2);
-      break;
-    }
-  }
-}
-
-template <bool WAIT>
-__global__ __launch_bounds__(256) void fwd_rows_kernel(const FwdDesc* __restrict__ descs, int32_t* err,
-                                                       uint64_t timeout) {
+__global__ __launch_bounds__(256) void fwd_rows_kernel(const FwdDesc* __restrict__ descs) {
   __shared__ __attribute__((aligned(16))) float sW1[HP * S_W1];
   __shared__ __attribute__((aligned(16))) float sW2[ZP * S_W2];
   __shared__ __attribute__((aligned(16))) float sW3[HP * S_W3];
@@ -76,7 +23,6 @@ __global__ __launch_bounds__(256) void fwd_rows_kernel(const FwdDesc* __restrict
 
   const FwdDesc d = descs[blockIdx.x];
   if (d.nrows <= 0) return;   // alignment filler of an XCD-grouped descriptor list (whole block)
-  if (WAIT && d.wait_seq != 0) block_wait_flag(d.wait_flag, d.wait_seq, err, timeout);
   if (fwd_compact_ok(d)) {
     stage_params<true>(d.params, sW1, sW2, sW3, sW4);
     __syncthreads();
@@ -149,11 +95,6 @@ __global__ __launch_bounds__(1024) void param_drift_kernel(const float* __restri
 // Layout probe: D = A*B for A[i][k] = i + 100k, B[k][j] = 1000k + j through
 // the documented lane maps; the host checks D against numpy (asymmetric B
 // catches a transposed C/D map).
-// the constant-rate clock the bounded waits use (s_memrealtime), for calibration
-__global__ void probe_realtime_kernel(uint64_t* out) {
-  if (threadIdx.x == 0) out[0] = __builtin_amdgcn_s_memrealtime();
-}
-
 __global__ void probe_mfma_kernel(float* out) {
   const int l = threadIdx.x;
   const float a = (float)((l & 15) + 100 * (l >> 4));
@@ -172,22 +113,8 @@ extern "C" {
 
 int fedmx_forward_rows(const void* descs, int nblocks, hipStream_t stream) {
   if (nblocks <= 0) return 0;
-  hipLaunchKernelGGL(fedmx::fwd_rows_kernel<false>, dim3(nblocks), dim3(256), 0, stream,
-                     reinterpret_cast<const fedmx::FwdDesc*>(descs), nullptr, (uint64_t)0);
-  return (int)hipGetLastError();
-}
-
-// early scoring: the start gate, then the forward whose blocks wait for their
-// model's done flag (FwdDesc::wait_seq / wait_flag); timeout in microseconds
-// (timeout in s_memrealtime ticks: ops/_hip.realtime_ticks_per_us calibrates the clock)
-int fedmx_forward_rows_wait(const void* descs, int nblocks, const int32_t* started, int32_t target, int32_t* err,
-                            int64_t timeout_ticks, hipStream_t stream) {
-  if (nblocks <= 0) return 0;
-  if (started == nullptr || timeout_ticks <= 0) return -1;
-  const uint64_t ticks = (uint64_t)timeout_ticks;
-  hipLaunchKernelGGL(fedmx::start_gate_kernel, dim3(1), dim3(64), 0, stream, started, target, err, ticks);
-  hipLaunchKernelGGL(fedmx::fwd_rows_kernel<true>, dim3(nblocks), dim3(256), 0, stream,
-                     reinterpret_cast<const fedmx::FwdDesc*>(descs), err, ticks);
+  hipLaunchKernelGGL(fedmx::fwd_rows_kernel, dim3(nblocks), dim3(256), 0, stream,
+                     reinterpret_cast<const fedmx::FwdDesc*>(descs));
   return (int)hipGetLastError();
 }
 
@@ -203,11 +130,6 @@ int fedmx_param_drift(const float* hist, int M, const float* newp, const int* se
                       hipStream_t stream) {
   if (M <= 0) return 0;
   hipLaunchKernelGGL(fedmx::param_drift_kernel, dim3(M), dim3(1024), 0, stream, hist, newp, seg, out);
-  return (int)hipGetLastError();
-}
-
-int fedmx_probe_realtime(uint64_t* out, hipStream_t stream) {
-  hipLaunchKernelGGL(fedmx::probe_realtime_kernel, dim3(1), dim3(64), 0, stream, out);
   return (int)hipGetLastError();
 }
 

@@ -17,8 +17,8 @@ struct FwdDesc {
   int32_t d_in;
   int32_t latent;
   int32_t hidden;
-  int32_t wait_seq;          // early scoring: wait until *wait_flag >= wait_seq (0: no wait)
-  const int32_t* wait_flag;  // the training kernel's done flag of this block's model (TrainArgs::done)
+  int32_t pad0;
+  int64_t pad1;
 };
 static_assert(sizeof(FwdDesc) == 64, "FwdDesc layout is shared with Python");
 

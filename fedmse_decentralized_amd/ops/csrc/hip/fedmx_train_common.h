@@ -36,28 +36,7 @@ struct TrainArgs {
   uint64_t* stamps;         // [8 waves][32] s_memtime stamps of one step (FEDMX_STAMPS builds), or null
   int32_t flags;            // TRAIN_FLAG_* bits
   int32_t pad0;
-  // Early scoring (engine/device_round.py): a kernel on another stream scores
-  // each client's model as soon as its workgroup has written it.  `started`
-  // counts workgroups that began (the scorer is only dispatched once every
-  // trainer is resident, so its spinning blocks can never keep a trainer off
-  // the CUs); done[store row] = seq once the row's parameters are visible at
-  // agent scope.  Both null: no signalling.
-  int32_t* started;
-  int32_t* done;
-  int32_t seq;
-  int32_t pad1;
 };
-
-// release this workgroup's parameter stores (every thread that wrote them has
-// executed __threadfence() before the barrier preceding this call)
-__device__ inline void signal_trained(const TrainArgs& A, int cid) {
-  if (A.done != nullptr && threadIdx.x == 0)
-    __hip_atomic_store(A.done + cid, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline void signal_started(const TrainArgs& A) {
-  if (A.started != nullptr && threadIdx.x == 0)
-    __hip_atomic_fetch_add(A.started, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 constexpr int32_t TRAIN_FLAG_NO_COMPACT = 1;  // identity-order kernels even where the compact order applies
 constexpr int32_t TRAIN_FLAG_HELPER = 2;      // helper-wave kernel (fedmx_train_hw.hip) for the compact shapes
 constexpr int32_t TRAIN_FLAG_NO_HELPER = 4;   // never the helper-wave kernel

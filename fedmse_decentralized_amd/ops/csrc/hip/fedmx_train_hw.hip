@@ -228,7 +228,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 
   const int kslot = blockIdx.x;
   const int cid = A.client_idx[kslot];
-  signal_started(A);
   float* const Pg = A.params + (size_t)cid * P_PAD;
   float* const Mg = A.adam_m + (size_t)cid * P_PAD;
   float* const Vg = A.adam_v + (size_t)cid * P_PAD;
@@ -1051,9 +1050,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   HSTAMP(true, 30);
   __syncthreads();
   masters_to_global_o<CP>(Pg, sW1, sW4, sW2, sW3);
-  if (A.done != nullptr) __threadfence();   // the parameters, at agent scope, before the signal
   __syncthreads();
-  signal_trained(A, cid);
   w1_to_lds(M, L);
   own_to_lds(M, L);
   __syncthreads();

@@ -28,7 +28,6 @@ VARIANTS = {
     "r0b0p": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=1"],  # pipelined tail only
     "r1b0": ["-DFEDMX_HW_REDUCE=1", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],  # grouped reads, unfenced
     "r0b0q": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=2"],  # tail in pipeline order, unfenced
-    "poll16": ["-DFEDMX_POLL_SLEEPS=16"],            # early scoring: poll a done flag every ~8 K clocks
     "packed": ["-DFEDMX_HW_PACKED=1"],               # packed-fp32 Adam (bit-identical)
     "abl_pf": ["-DFEDMX_HW_ABLATE=8"],               # timing only: prefetch always hits the cache
     "abl_hadam": ["-DFEDMX_HW_ABLATE=16"],           # timing only: helpers skip W4's Adam
