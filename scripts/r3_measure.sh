@@ -25,6 +25,6 @@ for f in $O/*.json; do python -c "import json; r=json.load(open('$f')); print('$
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$ROOT/$O/prof1" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 > "$ROOT/$O/prof1.log" 2>&1 || exit $?
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$ROOT/$O/prof8" -o run -- python3 "$ROOT/bench.py" --phantom-ranks 8 --steps 20 --warmup 5 > "$ROOT/$O/prof8.log" 2>&1 || exit $?
-python scripts/prof_summary.py $O/prof1/run_results.db --title "round 3: bench.py --steps 20 --warmup 3, 1x MI355X" --out $O/prof1.md > /dev/null
-python scripts/prof_summary.py $O/prof8/run_results.db --title "round 3: bench.py --phantom-ranks 8 (rank 0 of the 8-GPU job, collectives stubbed)" --out $O/prof8.md > /dev/null
+python "$ROOT/scripts/prof_summary.py" "$ROOT/$O/prof1/run_results.db" --title "round 3: bench.py --steps 20 --warmup 3, 1x MI355X" --out "$ROOT/$O/prof1.md" > /dev/null
+python "$ROOT/scripts/prof_summary.py" "$ROOT/$O/prof8/run_results.db" --title "round 3: bench.py --phantom-ranks 8 (rank 0 of the 8-GPU job, collectives stubbed)" --out "$ROOT/$O/prof8.md" > /dev/null
 echo done
