@@ -83,7 +83,7 @@ def fast_path_supported(fed) -> Optional[str]:
         (cfg.aggregation_mode in ("decentralized", "centralized"), f"aggregation mode {cfg.aggregation_mode}"),
         (cfg.protocol_variant == "code" or _thesis_fused_ok(fed),
          "thesis variant with verification rows beyond the fused kernel's LDS buffer"),
-        (fed.update_type in ("avg", "fedprox", "mse_avg"), f"update type {fed.update_type}"),
+        (fed.update_type in ("avg", "fedprox", "mse_avg", "fusion_avg"), f"update type {fed.update_type}"),
         (cfg.metric in ("AUC", "classification", "time"), f"metric {cfg.metric}"),
         # dropped clients leave at least one selection per round (k >= 1: the
         # election kernel needs a voter); larger drop sets take the host path
@@ -221,7 +221,13 @@ class DeviceRound:
         self.fused_verify = bool(fed.local) and max(int(d.shape[0]) for d in vdata) <= _hip.VERIFY_MAX_ROWS
         # aggregation weights: 1 = FedMSE 1/MSE (device), 0 = plain mean,
         # 2 = sample-weighted FedAvg (host-computed: they depend on the selection only)
-        self.rule = 1 if fed.update_type == "mse_avg" else (2 if cfg.fedavg_sample_weighted else 0)
+        # fusion_avg: weights formed on the device each round (rule 2 reads them
+        # from self.fw; Federation._fusion_weights_t, the host path's computation)
+        self.fusion = fed.update_type == "fusion_avg"
+        self.rule = 1 if fed.update_type == "mse_avg" else (2 if cfg.fedavg_sample_weighted or self.fusion else 0)
+        if self.fusion:
+            self.fstack = torch.zeros(max(N, 1), P_PAD, dtype=f32, device=dev)
+            self.fw = torch.zeros(max(N, 1), dtype=f32, device=dev)
         self.n_train = {c: fed.clients[c].train.shape[0] for c in range(N)}
         # protocol variants the kernels implement: majority election (every
         # selected client votes) and the centralised push (no verification)
@@ -458,7 +464,14 @@ class DeviceRound:
                                                                 noise if noise.size else np.zeros(1), rows)
                 rec_ptr, vec_ptr = 0, self.vec.data_ptr()
             hw_ptr = 0
-            if self.rule == 2:
+            if self.fusion:
+                # the selected models in selection order (device row gather from
+                # the model source the aggregation reads), then their weights
+                (sidx,) = self.rt.desc.put(np.asarray(rows, dtype=np.int32))
+                _hip.copy_rows(self.fstack.data_ptr(), P_PAD, 0, base.data_ptr(), P_PAD, sidx, k, P_PAD, dev)
+                self.fw[:k].copy_(fed._fusion_weights_t(self.fstack[:k]))
+                hw_ptr = self.fw.data_ptr()
+            elif self.rule == 2:
                 from ..protocol.aggregation import plan_mean
 
                 (hw_ptr,) = self.rt.desc.put(np.asarray([w for _, w in plan_mean(selected, self.n_train)],

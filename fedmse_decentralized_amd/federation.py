@@ -188,6 +188,7 @@ class Federation:
         self.fallback_rng = random.Random(cfg.data_seed + 7919 * (self.run + 1)) \
             if cfg.protocol_variant == "thesis" else None
         self._dev_kde = None
+        self._dev_kde_t = None   # (dev-row KDE scores, dev rows, padded -> canonical index) on the engine's device
         self.vstate: Dict[int, VerifierState] = {c: VerifierState() for c in self.local}
         self.versions: Dict[int, torch.Tensor] = {}
         self.last_received: List[Optional[int]] = [None] * N
@@ -410,12 +411,15 @@ class Federation:
                 if self.update_type == "mse_avg" and cfg.compat == "reference":
                     for _ in selected:          # calculate_mse_score per client (weights unused, Q3)
                         self.noise.rand()
-                sim = None
+                sim = fw = None
                 if self.update_type == "fusion_avg":
-                    sim = self._fusion_similarity(selected)
+                    if self._fusion_on_device():
+                        fw = self._fusion_weights_t(self._gather_params(list(selected), selected)).tolist()
+                    else:
+                        sim = self._fusion_similarity(selected)
                 ns = {c: self.clients[c].train.shape[0] for c in selected} if cfg.fedavg_sample_weighted else None
                 plan = make_plan(self.update_type, selected, aggregator, dev_mse, cfg.compat, sim=sim,
-                                 num_samples=ns)
+                                 num_samples=ns, fusion_w=fw)
             with self.tel.phase("comm"):
                 stack = self._gather_params([c for c, _ in plan], selected)
             with self.tel.phase("aggregate"):
@@ -550,6 +554,35 @@ class Federation:
         that of each selected model's reconstruction of it (host, subsampled
         to ``fusion_max_rows`` dev rows; identical on every rank)."""
         return self._fusion_similarity_of(self._gather_params(list(selected), selected), selected)
+
+    def _fusion_on_device(self) -> bool:
+        """The HIP engine forms the fusion weights on the GPU (torch, float64:
+        the same computation for the host-decision path and the device round)."""
+        return self.engine.name == "hip"
+
+    def _fusion_weights_t(self, stack: torch.Tensor) -> torch.Tensor:
+        """[k] float64 fusion_avg weights of the stacked models, on the stack's
+        device with no host round trip: each model's reconstruction of the
+        first ``fusion_max_rows`` dev rows, the JS distance of its KDE to the
+        dev set's, w ~ 1 / distance (utils.similarity ``*_t``)."""
+        from .models.layout import padded_index
+        from .models.reference import functional_forward, unflatten
+        from .utils.similarity import fusion_weights_t, js_distance_t, kde_log_density_t
+
+        dv = stack.device
+        if self._dev_kde_t is None or self._dev_kde_t[0].device != dv:
+            D = self.dims.d_in
+            rows = self.dev_set[: self.cfg.fusion_max_rows, :D].detach().to(dv, torch.float32).contiguous()
+            idx = padded_index(self.dims)[0].to(dv)   # once: a per-round host -> device copy would synchronise
+            self._dev_kde_t = (kde_log_density_t(rows), rows, idx)
+        kde, rows, idx = self._dev_kde_t
+        out = []
+        with torch.no_grad():
+            for i in range(stack.shape[0]):
+                t = unflatten(stack[i].float().index_select(-1, idx), self.dims)
+                _, y = functional_forward(t, rows)
+                out.append(js_distance_t(kde, kde_log_density_t(y)))
+            return fusion_weights_t(torch.stack(out))
 
     def _fusion_similarity_of(self, stack: torch.Tensor, ids: Sequence[int]) -> Dict[int, float]:
         from .models.layout import padded_to_canonical

@@ -63,10 +63,12 @@ def plan_mse_avg(selected: Sequence[int], aggregator: int, dev_mse: Dict[int, fl
     return [(cid, w / tot) for cid, w in raw]
 
 
-def plan_fusion(selected: Sequence[int], sim: Dict[int, float]) -> Plan:
+def plan_fusion(selected: Sequence[int], sim: Dict[int, float] = None, weights: Sequence[float] = None) -> Plan:
+    """``weights``: already formed (the HIP engine forms them on the device,
+    ``utils.similarity.fusion_weights_t``); else from the similarity scores."""
     from ..utils.similarity import fusion_weights
 
-    w = fusion_weights([sim[c] for c in selected])
+    w = weights if weights is not None else fusion_weights([sim[c] for c in selected])
     return [(cid, float(x)) for cid, x in zip(selected, w)]
 
 
@@ -74,11 +76,12 @@ UPDATE_TYPES = ("avg", "fedprox", "mse_avg", "fusion_avg")
 
 
 def make_plan(update_type: str, selected: Sequence[int], aggregator: int, dev_mse: Dict[int, float] = None,
-              compat: str = "reference", sim: Dict[int, float] = None, num_samples: Dict[int, float] = None) -> Plan:
+              compat: str = "reference", sim: Dict[int, float] = None, num_samples: Dict[int, float] = None,
+              fusion_w: Sequence[float] = None) -> Plan:
     if update_type in ("avg", "fedprox"):
         return plan_mean(selected, num_samples)
     if update_type == "mse_avg":
         return plan_mse_avg(selected, aggregator, dev_mse, compat)
     if update_type == "fusion_avg":
-        return plan_fusion(selected, sim)
+        return plan_fusion(selected, sim, fusion_w)
     raise ValueError(f"Unknown update type: {update_type}")

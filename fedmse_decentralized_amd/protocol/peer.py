@@ -122,10 +122,15 @@ class Peer:
                 eng.store.params[self.row].copy_(stack[i])
                 dev_mse[cid] = float(eng.model_mse([self.row], [fed.dev_set])[0])
             eng.store.params[self.row].copy_(saved)
-        sim = fed._fusion_similarity_of(stack, ids) if fed.update_type == "fusion_avg" else None
+        sim = fw = None
+        if fed.update_type == "fusion_avg":
+            if fed._fusion_on_device():
+                fw = fed._fusion_weights_t(stack).tolist()
+            else:
+                sim = fed._fusion_similarity_of(stack, ids)
         plan = make_plan(fed.update_type, list(range(len(ids))), self.client_id,
                          {i: dev_mse[c] for i, c in enumerate(ids)} if dev_mse else None, "fixed",
-                         sim={i: sim[c] for i, c in enumerate(ids)} if sim else None)
+                         sim={i: sim[c] for i, c in enumerate(ids)} if sim else None, fusion_w=fw)
         return eng.weighted_sum(stack[[i for i, _ in plan]], [w for _, w in plan])
 
     def aggregate_models(self, selected: Sequence["Peer"]) -> Optional[torch.Tensor]:

@@ -18,9 +18,16 @@ dev set (small JS distance) gets a large weight, ``w_k ∝ 1 / (s_k + eps)``.
 KDE on the host is quadratic in the number of rows, so callers subsample
 (``ExperimentConfig.fusion_max_rows``).  No reference fixture pins the
 numbers ("parity unpinned"); tests check the closed forms and invariants.
+
+The ``*_t`` functions are the same computations in torch (float64, on any
+device): the HIP engine's form, which runs on the GPU with the round's other
+work (no host round trip, so the device-resident round protocol can use it):
+the exact Gaussian-kernel sum instead of sklearn's tree (which, with its
+default zero tolerances, sums the same terms), scipy's JS distance formula.
 """
 from __future__ import annotations
 
+import math
 from typing import Sequence
 
 import numpy as np
@@ -71,3 +78,49 @@ def fusion_weights(sim_scores: Sequence[float], eps: float = 1e-12) -> np.ndarra
     if not np.isfinite(tot) or tot <= 0:
         return np.full(len(s), 1.0 / max(len(s), 1))
     return inv / tot
+
+
+# ---- torch (device) forms ------------------------------------------------------
+
+def kde_log_density_t(x):
+    """``kde_log_density`` in torch float64: Scott bandwidth n^(-1/(d+4)),
+    log of the mean normalised Gaussian kernel over all rows (self included)."""
+    import torch
+
+    x = x.to(torch.float64)
+    n, d = x.shape
+    h = float(n) ** (-1.0 / (d + 4))
+    d2 = torch.cdist(x, x, compute_mode="donot_use_mm_for_euclid_dist").square()
+    log_norm = 0.5 * d * math.log(2.0 * math.pi) + d * math.log(h) + math.log(n)
+    return torch.logsumexp(d2 * (-0.5 / (h * h)), dim=1) - log_norm
+
+
+def js_distance_t(log_p, log_q):
+    """scipy.spatial.distance.jensenshannon(exp(log_p), exp(log_q)) (natural
+    log) in torch: both normalised to sum 1, sqrt of the mean of the two
+    relative entropies to the midpoint."""
+    import torch
+
+    n = min(log_p.shape[0], log_q.shape[0])
+    p = torch.exp(log_p[:n].to(torch.float64))
+    q = torch.exp(log_q[:n].to(torch.float64))
+    p = p / p.sum()
+    q = q / q.sum()
+    m = (p + q) / 2.0
+
+    def rel_entr(a, b):
+        return torch.where(a > 0, a * torch.log(a / b), torch.zeros_like(a))
+
+    return torch.sqrt((rel_entr(p, m).sum() + rel_entr(q, m).sum()) / 2.0)
+
+
+def fusion_weights_t(sim_scores, eps: float = 1e-12):
+    """``fusion_weights`` in torch, without a host decision: uniform weights
+    when the inverse scores do not sum to a positive finite value."""
+    import torch
+
+    s = sim_scores.to(torch.float64)
+    inv = 1.0 / (torch.where(torch.isfinite(s), s, torch.full_like(s, math.inf)) + eps)
+    tot = inv.sum()
+    ok = torch.isfinite(tot) & (tot > 0)
+    return torch.where(ok, inv / tot, torch.full_like(inv, 1.0 / max(int(s.numel()), 1)))

@@ -462,8 +462,10 @@ def _worker_kw(rank, world, port, out, kw):
     from fedmse_decentralized_amd.parallel.launch import init_comm, shutdown
 
     comm = init_comm(backend="gloo", device="cuda")
+    kw = dict(kw)
+    ut = kw.pop("_update", "mse_avg")
     fed, res = _run(_cfg(os.path.join(out, f"r{rank}"), save_checkpoints=False, debug_replica_check=True, **kw),
-                    "mse_avg", 4, comm=comm)
+                    ut, 4, comm=comm)
     res["fast"] = fed._fast is not None
     res["params"] = fed.engine.store.params.double().sum(1).tolist()
     res["local"] = fed.local
@@ -478,7 +480,9 @@ def _worker_kw(rank, world, port, out, kw):
                                 dict(aggregation_mode="centralized", dropped_clients=[2]),
                                 # poisoned updates: receivers on both ranks reject, and every
                                 # side slot is reused (4 rounds > 3 slots) with fresh counts
-                                dict(malicious_clients=[1, 4], malicious_scale=25.0)])
+                                dict(malicious_clients=[1, 4], malicious_scale=25.0),
+                                # fusion weights formed on each rank's GPU from the gathered models
+                                dict(_update="fusion_avg", fusion_max_rows=256)])
 def test_device_round_variants_multi_rank_one_gpu(tmp_path, kw):
     """Protocol variants on the device path with two gloo ranks sharing one
     GPU: every rank reaches the single-process run's decisions, metrics and
@@ -486,7 +490,9 @@ def test_device_round_variants_multi_rank_one_gpu(tmp_path, kw):
     out = str(tmp_path)
     mp.start_processes(_worker_kw, args=(2, _port(), out, kw), nprocs=2, join=True, start_method="spawn")
     _shrink()
-    fed, ref = _run(_cfg(os.path.join(out, "single"), save_checkpoints=False, **kw), "mse_avg", 4)
+    kw = dict(kw)
+    ut = kw.pop("_update", "mse_avg")
+    fed, ref = _run(_cfg(os.path.join(out, "single"), save_checkpoints=False, **kw), ut, 4)
     ref_params = fed.engine.store.params.double().sum(1).tolist()
     for r in range(2):
         d = json.load(open(os.path.join(out, f"rank{r}.json")))
@@ -496,3 +502,16 @@ def test_device_round_variants_multi_rank_one_gpu(tmp_path, kw):
             np.testing.assert_array_equal(np.array(x), np.array(y))
         loc = d["local"]
         assert d["params"] == ref_params[loc[0]:loc[-1] + 1]
+
+
+def test_device_round_fusion_avg_matches_host_path(tmp_path):
+    """fusion_avg on the device round: the KDE / JS weights formed on the GPU
+    each round (no host round trip) give the host-decision path's rounds."""
+    _shrink()
+    kw = dict(save_checkpoints=False, fusion_max_rows=256)
+    fa, a = _run(_cfg(str(tmp_path / "dev"), device_protocol=True, update_types=["fusion_avg"], **kw), "fusion_avg", 4)
+    fb, b = _run(_cfg(str(tmp_path / "host"), device_protocol=False, update_types=["fusion_avg"], **kw),
+                 "fusion_avg", 4)
+    assert fa._fast is not None and fb._fast is None
+    assert a == b
+    assert torch.equal(fa.engine.store.params, fb.engine.store.params)

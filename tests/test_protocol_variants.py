@@ -79,6 +79,24 @@ def test_similarity_score_and_fusion_weights():
     assert abs(w.sum() - 1) < 1e-12 and w[0] > w[1]
 
 
+def test_torch_similarity_forms_match_sklearn_scipy():
+    """The device (torch float64) KDE / JS / weights against sklearn + scipy."""
+    rng = np.random.default_rng(3)
+    dev = rng.normal(size=(300, 6))
+    recs = [dev + 0.05 * rng.normal(size=dev.shape), 2.0 * rng.normal(size=dev.shape) + 1.0,
+            dev[::-1] * 0.9]
+    kd = sim.kde_log_density(dev)
+    kd_t = sim.kde_log_density_t(torch.from_numpy(dev))
+    np.testing.assert_allclose(kd_t.numpy(), kd, rtol=1e-11, atol=1e-9)
+    ref = [sim.similarity_score(kd, r) for r in recs]
+    got = [float(sim.js_distance_t(kd_t, sim.kde_log_density_t(torch.from_numpy(r)))) for r in recs]
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(sim.fusion_weights_t(torch.tensor(got, dtype=torch.float64)).numpy(), sim.fusion_weights(ref), rtol=1e-9)
+    # degenerate scores fall back to uniform weights, as the numpy form
+    bad = torch.tensor([float("nan"), float("inf")], dtype=torch.float64)
+    np.testing.assert_array_equal(sim.fusion_weights_t(bad).numpy(), sim.fusion_weights([np.nan, np.inf]))
+
+
 SMALL = dict(normal_rows=(90, 100), abnormal_rows=(120, 130), test_normal_rows=20)
 
 
