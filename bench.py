@@ -143,8 +143,10 @@ def _measure(fed, comm, device, steps: int, warmup: int, profile):
     r0 = fed.round_idx
     t0 = time.perf_counter()
     last = None
+    results = []
     for _ in range(steps):
         last = one_round()
+        results.append(last)
     fed.finish()         # device-protocol rounds: collect results, hand reports to the writer
     fed.writer.flush()   # artefacts of the timed rounds are on disk before the clock stops
     if prof is not None:
@@ -168,7 +170,17 @@ def _measure(fed, comm, device, steps: int, warmup: int, profile):
     if fr is not None and getattr(fr, "train_timing", False):
         mine = torch.tensor([fr.train_ms.get(r, 0.0) for r in range(r0, r0 + steps)], dtype=torch.float64)
         train_ms = comm.all_gather(mine).reshape(comm.world_size, steps).numpy()
-    return dt, last, train_ms
+    # local epochs the trained clients actually ran in the timed rounds
+    # (validation early stopping, patience 1): the work behind ms_per_step
+    # (read after the clock: the device-protocol rounds are collected by now)
+    ep = [0.0, 0.0]
+    for res in results:
+        e = getattr(res, "epochs_run", None) or {}
+        ep[0] += float(sum(e.values()))
+        ep[1] += float(len(e))
+    tot = comm.all_gather(torch.tensor(ep, dtype=torch.float64)).reshape(comm.world_size, 2).sum(0)
+    epochs_mean = float(tot[0] / tot[1]) if float(tot[1]) > 0 else None
+    return dt, last, train_ms, epochs_mean
 
 
 def _main(argv, real_stdout: int):
@@ -245,7 +257,7 @@ def _main(argv, real_stdout: int):
     time_train = n_gpus > 1 and fed._fast is not None
     if time_train:
         fed._fast.train_timing = True
-    dt, last, train_ms = _measure(fed, comm, device, args.steps, args.warmup, args.profile)
+    dt, last, train_ms, epochs_mean = _measure(fed, comm, device, args.steps, args.warmup, args.profile)
     fed_rps = args.steps / dt
     # whole-job value: with the default 10 clients per GPU the federation has
     # 10*N clients and the job does N 10-client federations' worth of work
@@ -297,6 +309,9 @@ def _main(argv, real_stdout: int):
                 "device_protocol": fed._fast is not None,
             },
             "federation_rounds_per_sec": round(fed_rps, 4),
+            # of config.local_epochs: clients stop early once their validation
+            # loss stops improving (patience 1), so the work per round varies
+            "local_epochs_run_mean": None if epochs_mean is None else round(epochs_mean, 3),
             "detection_auc_mean": round(auc, 6),
             "detection_auc_min": round(auc_min, 6),
             "phase_ms_total": {k: round(v, 3) for k, v in fed.tel.summary().items()},
@@ -327,7 +342,7 @@ def _main(argv, real_stdout: int):
         # beside the weak-scaling headline, not folded into it
         fed.finish()
         fed10 = build(10)
-        dt10, last10, _ = _measure(fed10, comm, device, args.steps, args.warmup, None)
+        dt10, last10, _, _ = _measure(fed10, comm, device, args.steps, args.warmup, None)
         if rec is not None:
             m10 = np.asarray(last10.metrics, dtype=np.float64)
             rec["strong_scaling_10_clients"] = {
