@@ -206,6 +206,8 @@ def _main(argv, real_stdout: int):
                    help="synthetic feature family (BASELINE config 5 uses kitsune, non-IID)")
     p.add_argument("--non-iid", action="store_true", help="Dirichlet non-IID client mixtures")
     p.add_argument("--compat", default="fixed")
+    p.add_argument("--init-mode", default="auto", choices=["auto", "shared", "per_client"],
+                   help="initial client models (auto: shared under compat fixed, see config.init_mode)")
     p.add_argument("--no-artifacts", action="store_true", help="skip model.cpt/tracking/JSONL writes")
     p.add_argument("--trace", default=None, help="per-phase JSONL trace (adds device syncs)")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
@@ -243,7 +245,7 @@ def _main(argv, real_stdout: int):
             model_types=[args.model_type], update_types=[args.update_type],
             synthetic=args.data_kind, synthetic_iid=not args.non_iid, compat=args.compat, backend=args.backend,
             global_early_stop=False, save_checkpoints=not args.no_artifacts, output_root=out_root,
-            trace_file=args.trace, log_level="WARNING")
+            trace_file=args.trace, log_level="WARNING", init_mode=args.init_mode)
         fed = Federation(cfg, args.model_type, args.update_type, run=0, comm=comm,
                          write_reports=not args.no_artifacts).setup()
         if phantom and fed._fast is None:
