@@ -66,8 +66,18 @@
 #define FEDMX_HW_BIASX 0
 #endif
 // issue priority of the main waves over their helpers (s_setprio level; 0: equal)
+// helpers sleep ~64 x N clocks after barrier #2 before their dW4 MFMAs (so
+// they do not contend for the matrix pipe with the mains' dZ / dH1 chain);
+// 0: no delay
+#ifndef FEDMX_HW_HDELAY
+#define FEDMX_HW_HDELAY 0
+#endif
 #ifndef FEDMX_HW_PRIO
 #define FEDMX_HW_PRIO 0
+#endif
+// issue priority of the helpers over their main waves (s_setprio level; 0: equal)
+#ifndef FEDMX_HW_HPRIO
+#define FEDMX_HW_HPRIO 0
 #endif
 
 namespace fedmx {
@@ -515,6 +525,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   if (helper) {
     // =========================== helper waves ===================================
     if (FEDMX_HW_PRIO) __builtin_amdgcn_s_setprio(0);
+    if (FEDMX_HW_HPRIO) __builtin_amdgcn_s_setprio(FEDMX_HW_HPRIO);
     HSlab P4, M4, V4, AN4;
     stage_vals(pv_m);
     lds_to_hslab(M4, L);
@@ -580,6 +591,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         const f32x4 w4a1 = lds_read4(sT0 + tr + 16 * S_T);
         const f32x4 w4b0 = lds_read4(sT1 + tr);
         const f32x4 w4b1 = lds_read4(sT1 + tr + 16 * S_T);
+        if (FEDMX_HW_HDELAY > 0) __builtin_amdgcn_s_sleep(FEDMX_HW_HDELAY);
         f32x4 G4[2][2];
 #pragma unroll
         for (int v = 0; v < 2; ++v)

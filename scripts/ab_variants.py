@@ -28,6 +28,12 @@ VARIANTS = {
     "r0b0p": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=1"],  # pipelined tail only
     "r1b0": ["-DFEDMX_HW_REDUCE=1", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],  # grouped reads, unfenced
     "r0b0q": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=2"],  # tail in pipeline order, unfenced
+    # r3: helper-side timing probes (train launch us, base 945 / 947 on the same box)
+    "hd8": ["-DFEDMX_HW_HDELAY=8"],                  # helpers wait ~512 clocks before dW4   1049 (+11 %)
+    "hd16": ["-DFEDMX_HW_HDELAY=16"],                # ~1 K clocks                           1064
+    "hd24": ["-DFEDMX_HW_HDELAY=24"],                # ~1.5 K clocks                         1088
+    "hprio1": ["-DFEDMX_HW_HPRIO=1"],                # helpers at issue priority 1 over the mains   1071 (+13 %)
+    "hprio3": ["-DFEDMX_HW_HPRIO=3"],                # helpers at issue priority 3                  1070
     "packed": ["-DFEDMX_HW_PACKED=1"],               # packed-fp32 Adam (bit-identical)
     "abl_pf": ["-DFEDMX_HW_ABLATE=8"],               # timing only: prefetch always hits the cache
     "abl_hadam": ["-DFEDMX_HW_ABLATE=16"],           # timing only: helpers skip W4's Adam
