@@ -34,7 +34,7 @@ VARIANTS = {
     "hd24": ["-DFEDMX_HW_HDELAY=24"],                # ~1.5 K clocks                         1088
     "hprio1": ["-DFEDMX_HW_HPRIO=1"],                # helpers at issue priority 1 over the mains   1071 (+13 %)
     "hprio3": ["-DFEDMX_HW_HPRIO=3"],                # helpers at issue priority 3                  1070
-    "packed": ["-DFEDMX_HW_PACKED=1"],               # packed-fp32 Adam (bit-identical)
+    "packed": ["-DFEDMX_HW_PACKED=1"],               # packed-fp32 Adam (bit-identical)  966-974 vs 948-951 (+2 %)
     "abl_pf": ["-DFEDMX_HW_ABLATE=8"],               # timing only: prefetch always hits the cache
     "abl_hadam": ["-DFEDMX_HW_ABLATE=16"],           # timing only: helpers skip W4's Adam
     "abl_madam": ["-DFEDMX_HW_ABLATE=32"],           # timing only: mains skip W1's Adam
