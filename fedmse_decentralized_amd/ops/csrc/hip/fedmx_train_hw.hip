@@ -79,23 +79,6 @@
 #ifndef FEDMX_HW_HPRIO
 #define FEDMX_HW_HPRIO 0
 #endif
-// 1: Gram-form step (round 3).  Layer 4, dY, the loss and dW4 run on the
-// helper waves; the main waves get dH3 without a cross-wave reduction:
-//   dH3 = W4^T dY = s * (G H3 - W4^T X),   G = W4^T W4,  s = 2 / (bt * d_in)
-// (dY = s (W4 H3 - X) on the real rows / batch columns; W4's padding rows and
-// X's padding columns are zero, so G and W4^T X need no masks).  G (32 x 32,
-// symmetric) and W4^T X (32 x batch) depend only on W4(s) and the chunk: after
-// W4's Adam update the helpers publish W4^T to LDS, and between barriers #1
-// and #2 of the next step -- while the mains run layers 1-3 and the matrix
-// pipe is mostly idle -- each helper forms whole pre-scaled tiles of them
-// (40 MFMAs each).  Barrier #2 now sits right after layer 3; after it every
-// main wave forms dH3 with 14 MFMAs from its own H3.  The mains' chain loses
-// layer 4, dY and the dH3 partial + barrier + reduction.  (A first version
-// formed per-helper partial sums after W4's Adam and reduced them after
-// barrier #1: the helpers' path became critical, +19 %; profiles/r3_gram_*.)
-#ifndef FEDMX_HW_GRAM
-#define FEDMX_HW_GRAM 0
-#endif
 
 namespace fedmx {
 namespace hw {
@@ -123,8 +106,7 @@ constexpr int L_T32 = 32 * S_T;          // 640
 constexpr int L_T16 = 16 * S_T;          // 320
 constexpr int L_SCR = 4 * L_T32 + 2 * L_T16;  // 3200 per main wave (dY^T, H3^T, H1^T, dH3^T | Z^T, dZ^T)
 constexpr int L_Q4 = 4 * 4 * 64 * 4;     // 4096 W4 rows in the dH3 A-operand layout [w][v][t][lane][4]
-constexpr int L_W4T = HP * S_W1;         // 4224 Gram form: W4^T
-constexpr int L_TOTAL = L_W1 + L_W4 + L_W2 + L_W3 + 3 * L_RED + 4 * L_SCR + L_Q4 + 128 + L_W4T;
+constexpr int L_TOTAL = L_W1 + L_W4 + L_W2 + L_W3 + 3 * L_RED + 4 * L_SCR + L_Q4 + 128;
 static_assert(L_TOTAL * 4 <= 160 * 1024, "LDS budget");
 
 // main-wave optimizer state: W1 column block (MFMA A-operand layout) + small tile
@@ -233,14 +215,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // per-step Adam scalars (helper -> main), double-buffered by step parity:
   // [neg_step_size, inv_bc2s, bc2s, -]
   float* const sK = reinterpret_cast<float*>(sLoss + 32);
-  // Gram form (FEDMX_HW_GRAM): the dH3-reduction and W4-copy areas hold the
-  // helpers' partial sums and their reductions; main w's dY^T slot holds its H3
-  // in the D layout (the helper's layer-4 operand)
-  float* const sGR = sQ4;                 // [tile 2t'+t][lane][4]  s G (D layout)
-  float* const sXP = sQ4 + 4 * 256;       // [helper][lane][4]      -s W4^T X tile 0, partials
-  float* const sXR1 = sQ4 + 8 * 256;      // [lane][4]              -s W4^T X tile 1
-  float* const sW4T = sQ4 + L_Q4 + 128;   // [h][S_W1]              W4(s)^T
-  float* const sH3D = sT0;                // [t][lane][4]           H3 (main w)
 
   Lane L;
   L.w1 = sW1 + c * S_W1 + 32 * w + 4 * g;
@@ -573,6 +547,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         for (int t = 0; t < 2; ++t)
           lds_write4(q4p + (2 * v + t) * 256, f32x4{P4.q4[v][t][0], P4.q4[v][t][1], P4.q4[v][t][2], P4.q4[v][t][3]});
     };
+    publish_q4();
     // The step's Adam scalars (f64 bias corrections: ~6 % of the main waves'
     // step when they computed them, FEDMX_HW_ABLATE=1) are formed here one
     // step ahead and handed over through LDS.
@@ -582,212 +557,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       if (lane == 0 && w8 == 4)
         lds_write4(sK + 4 * (js & 1), f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f});
     };
-#if FEDMX_HW_GRAM
-    // W4(s) transposed ([h][d], stride S_W1): this helper's 32 columns d, one
-    // 16-byte write per (v, t) from the register-held D-layout rows
-    auto publish_w4t = [&]() {
-#pragma unroll
-      for (int v = 0; v < 2; ++v)
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          lds_write4(sW4T + (16 * t + c) * S_W1 + 32 * w + 16 * v + 4 * g,
-                     f32x4{P4.q4[v][t][0], P4.q4[v][t][1], P4.q4[v][t][2], P4.q4[v][t][3]});
-    };
-    // The chunk's X rows in the f layout over all 128 columns, 16-column block
-    // kp at xw[kp] (helper 3: all eight blocks; helpers 0-2: blocks 2w, 2w+1 at
-    // xw[0], xw[1]) -- the B operand of W4^T X -- and the b layout (dY).
-    f32x4 xw[8];
-    float xb0[4], xb1[4], nb0[4], nb1[4];
-    auto load_x = [&](int row0, int bc, float (&b0)[4], float (&b1)[4]) {
-      const float* src = Xtr + (size_t)(row0 + ((unsigned)brow_c < (unsigned)bc ? brow_c : 0)) * DP + 4 * g;
-      if (w == 3) {
-#pragma unroll
-        for (int kp = 0; kp < 8; ++kp) xw[kp] = *reinterpret_cast<const f32x4*>(src + 16 * kp);
-      } else {
-        xw[0] = *reinterpret_cast<const f32x4*>(src + 32 * w);
-        xw[1] = *reinterpret_cast<const f32x4*>(src + 32 * w + 16);
-      }
-      const float* bsrc = Xtr + (size_t)row0 * DP + 32 * w + c;
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const int rr = ((unsigned)brow_b[r] < (unsigned)bc) ? brow_b[r] : 0;
-        b0[r] = bsrc[(size_t)rr * DP];
-        b1[r] = bsrc[(size_t)rr * DP + 16];
-      }
-      b0[3] = 0.f;
-      b1[3] = 0.f;
-    };
-    // Between barriers #1 and #2 (the mains run layers 1-3; the matrix pipe is
-    // mostly idle) each helper forms whole tiles over all 128 rows of W4(s)
-    // from the transposed masters, pre-scaled by the step's dY scale s:
-    //   helper 0: s G(0,0)   helper 1: s G(1,1)   helper 2: s G(0,1) and (1,0)
-    //   helper 3: -s W4^T X tile 1;  every helper: -s W4^T X tile 0 over its
-    //   two 16-column blocks (four partials, summed by the mains).
-    auto gram_tiles = [&](float scale) {
-      const float* ra = sW4T + ((w & 1) ? 16 + c : c) * S_W1 + 4 * g;   // A rows (G, W4^T X tile 1)
-      const float* r0 = sW4T + c * S_W1 + 4 * g;                        // rows of tile 0
-      f32x4 acc = zero4(), xp = zero4();
-      if (w == 3) {
-#pragma unroll
-        for (int kp = 0; kp < 8; ++kp) {
-          const f32x4 a = lds_read4(ra + 16 * kp);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma16(a[s], xw[kp][s], acc);
-          if (kp >= 6) {
-            const f32x4 a0 = lds_read4(r0 + 16 * kp);
-#pragma unroll
-            for (int s = 0; s < 4; ++s) xp = mfma16(a0[s], xw[kp][s], xp);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = -(acc[r] * scale);
-        lds_write4(sXR1 + lane * 4, acc);
-      } else {
-        const float* rb = sW4T + (w == 0 ? c : 16 + c) * S_W1 + 4 * g;
-#pragma unroll
-        for (int kp = 0; kp < 8; ++kp) {
-          const f32x4 a = lds_read4(ra + 16 * kp);
-          const f32x4 b = (w == 2) ? lds_read4(rb + 16 * kp) : a;
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const f32x4 a0 = lds_read4(r0 + 16 * (2 * w + j));
-#pragma unroll
-          for (int s = 0; s < 4; ++s) xp = mfma16(a0[s], xw[j][s], xp);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = acc[r] * scale;
-        lds_write4(sGR + (w == 0 ? 0 : (w == 1 ? 3 : 1)) * 256 + lane * 4, acc);
-        if (w == 2) {
-          // lane (c, g) reg r holds G[4g+r][16+c] = G[16+c][4g+r]: tile (1,0)'s
-          // lane ((c>>2)*16 + 4g + r), reg c&3
-#pragma unroll
-          for (int r = 0; r < 4; ++r) sGR[2 * 256 + ((c >> 2) * 16 + 4 * g + r) * 4 + (c & 3)] = acc[r];
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) xp[r] = -(xp[r] * scale);
-      lds_write4(sXP + w * 256 + lane * 4, xp);
-    };
-    publish_w4t();
-    if (nb > 0) load_x(0, min(B, n_tr), xb0, xb1);
-    publish_k();   // step 0's
-    for (int ep = 0; ep < A.epochs; ++ep) {
-      double acc_tr = 0.0;
-      for (int bi = 0; bi < nb; ++bi) {
-        const bool hs = (ep == 0 && bi == STAMP_STEP);
-        const int bt = min(B, n_tr - bi * B);
-        const float scale = 2.0f / (float)(bt * d_in);
-        HSTAMP(hs, 0);
-        __syncthreads();   // barrier #1 (W4(s)^T published)
-        HSTAMP(hs, 2);
-        if (!(FEDMX_HW_ABLATE & 256)) gram_tiles(scale);
-        // W4(s) rows as layer 4's B operand (own rows, written by this wave)
-        const f32x4 a00 = lds_read4(a4p);
-        const f32x4 a01 = lds_read4(a4p + 16);
-        const f32x4 a10 = lds_read4(a4p + 16 * S_W4);
-        const f32x4 a11 = lds_read4(a4p + 16 * S_W4 + 16);
-        HSTAMP(hs, 6);
-        __syncthreads();   // barrier #2 (main: H3 written; helpers: G(s), W4^T X(s))
-        HSTAMP(hs, 7);
-        {
-          // the next chunk (after an epoch's last step: the next epoch's first)
-          const int row_n = bi + 1 < nb ? (bi + 1) * B : 0;
-          load_x(row_n, min(B, n_tr - row_n), nb0, nb1);
-        }
-        if (FEDMX_HW_ABLATE & 512) {   // timing only: no layer 4 / dW4 / Adam on the helpers
-          publish_w4t();
-          ++js;
-          publish_k();
-          continue;
-        }
-        const f32x4 h3d0 = lds_read4(sH3D + lane * 4);
-        const f32x4 h3d1 = lds_read4(sH3D + 256 + lane * 4);
-        const f32x4 h3t0 = lds_read4(sT1 + tr);
-        const f32x4 h3t1 = lds_read4(sT1 + tr + 16 * S_T);
-        // ---- layer 4, transposed: Y^T[batch pos][own row d] (A = H3 in the D
-        // layout, B = W4^T), so dY comes out as dW4's A operand
-        f32x4 yt0 = zero4(), yt1 = zero4();
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          yt0 = mfma16(h3d0[s], a00[s], yt0);
-          yt1 = mfma16(h3d0[s], a10[s], yt1);
-        }
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          yt0 = mfma16(h3d1[s], a01[s], yt0);
-          yt1 = mfma16(h3d1[s], a11[s], yt1);
-        }
-        // ---- dY (masked: padding batch positions, X's bias column) and the loss
-        f32x4 dyt[2];
-        float sq = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool ok = (unsigned)brow_b[r] < (unsigned)bt;
-          const float d0 = ok ? yt0[r] - xb0[r] : 0.f;
-          const float d1 = (ok && !bias_col) ? yt1[r] - xb1[r] : 0.f;
-          sq += d0 * d0 + d1 * d1;
-          dyt[0][r] = d0 * scale;
-          dyt[1][r] = d1 * scale;
-        }
-        if (!(FEDMX_HW_ABLATE & 2)) acc_tr += (double)(sq * ((1.0f / (float)bt) * inv_d));
-        HSTAMP(hs, 8);
-        // ---- dW4 (own rows) = dY H3^T over the batch
-        f32x4 G4[2][2];
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-#pragma unroll
-          for (int t = 0; t < 2; ++t) G4[v][t] = zero4();
-#pragma unroll
-        for (int s = 0; s < KB; ++s) {
-          G4[0][0] = mfma16(dyt[0][s], h3t0[s], G4[0][0]);
-          G4[0][1] = mfma16(dyt[0][s], h3t1[s], G4[0][1]);
-          G4[1][0] = mfma16(dyt[1][s], h3t0[s], G4[1][0]);
-          G4[1][1] = mfma16(dyt[1][s], h3t1[s], G4[1][1]);
-        }
-        float prox_acc = 0.f;
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            if (FEDMX_HW_PACKED && !PROX)
-              adam4_packed(P4.q4[v][t], M4.q4[v][t], V4.q4[v][t], G4[v][t], K);
-            else
-              adam4<PROX>(P4.q4[v][t], M4.q4[v][t], V4.q4[v][t], AN4.q4[v][t], G4[v][t], K, prox_acc);
-          }
-        if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
-        HSTAMP(hs, 10);
-        publish_w4t();      // W4(s+1)^T: the next step's G / W4^T X
-        w4_to_lds(P4, L);   // W4(s+1) master rows (own layer 4, validation, snapshots)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          xb0[r] = nb0[r];
-          xb1[r] = nb1[r];
-        }
-        ++js;
-        if (!(FEDMX_HW_ABLATE & 128)) publish_k();   // step js's scalars, read by the mains after its barrier #1
-        HSTAMP(hs, 11);
-      }
-      double prox_now = 0.0;
-      if (PROX) {
-        float pr = 0.f;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int v = 0; v < 2; ++v) {
-              const float d4 = P4.q4[v][t][r] - AN4.q4[v][t][r];
-              pr += d4 * d4;
-            }
-        prox_now = (double)pr;
-      }
-      if (epoch_tail(ep, acc_tr, prox_now)) break;
-    }
-#else
-    publish_q4();
     publish_k();   // step 0's
     AdamStep KN = K;   // FEDMX_HW_KEARLY: the next step's scalars
     for (int ep = 0; ep < A.epochs; ++ep) {
@@ -879,7 +648,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
       if (epoch_tail(ep, acc_tr, prox_now)) break;
     }
-#endif
     // write back (barriers as the main branch; the mains stage to global)
     __syncthreads();
     __syncthreads();
@@ -969,13 +737,11 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           K.bc2s = kk[2];
           ++js;
         }
-#if !FEDMX_HW_GRAM
         // W4(s) rows in the dH3 A-operand layout (helper-published)
 #pragma unroll
         for (int v = 0; v < 2; ++v)
 #pragma unroll
           for (int t = 0; t < 2; ++t) q4[v][t] = lds_read4(q4p + (2 * v + t) * 256);
-#endif
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           f32x4 s = lds_read4(red + t * 256 + lane * 4);
@@ -1019,81 +785,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           h3[0] = acc0;
           h3[1] = acc1;
         }
-#if FEDMX_HW_GRAM
-        // H3 for the helper: D layout (its layer-4 A operand) and transposed
-        // (its dW4 B operand)
-        lds_write4(sH3D + lane * 4, h3[0]);
-        lds_write4(sH3D + 256 + lane * 4, h3[1]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          sT1[tw + r * S_T] = h3[0][r];
-          sT1[tw + (16 + r) * S_T] = h3[1][r];
-        }
-        const bool col_ok = (unsigned)brow_c < (unsigned)bt;
-        float nz = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) nz += zreal_d[r] ? z[r] * z[r] : 0.f;
-        nz = sum_lane_groups(nz);
-        norm_c = __builtin_amdgcn_sqrtf(nz);
-        // the reconstruction loss is the helpers' (they form Y); here the shrink term
-        if (!(FEDMX_HW_ABLATE & 2) && w == 0 && g == 0 && col_ok) acc_tr += (double)(lam * norm_c * inv_bt);
-        HSTAMP(ms, 3);
-      }
-      if (has_next) load_chunk(Xtr, (FEDMX_HW_ABLATE & 8) ? 0 : row_n, bc_n, nxt);  // prefetch (ablation 8: chunk 0, cached)
-
-      float q2[2][4], q3[2][4];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          q2[t][r] = d2p[r * S_W2 + 16 * t];
-          q3[t][r] = d3p[(16 * t + r) * S_W3];
-        }
-      const bool col_ok = (unsigned)brow_c < (unsigned)bt;
-      HSTAMP(ms, 4);
-      __syncthreads();  // barrier #2: H3 published; s G(s) and -s W4^T X(s) reduced
-      HSTAMP(ms, 7);
-      // ---- dH3 = s G H3 - s W4^T X (A operand: G's D-layout tile (t', t) is,
-      // by symmetry, the A operand of output tile t at k-block t')
-      f32x4 dh3[2];
-      {
-        f32x4 gt[2][2];
-#pragma unroll
-        for (int tp = 0; tp < 2; ++tp)
-#pragma unroll
-          for (int t = 0; t < 2; ++t) gt[tp][t] = lds_read4(sGR + (2 * tp + t) * 256 + lane * 4);
-        f32x4 acc0 = lds_read4(sXP + lane * 4), acc1 = lds_read4(sXR1 + lane * 4);
-#pragma unroll
-        for (int hw = 1; hw < 4; ++hw) {
-          const f32x4 o = lds_read4(sXP + hw * 256 + lane * 4);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc0[r] = acc0[r] + o[r];
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          acc0 = mfma16(gt[0][0][s], h3[0][s], acc0);
-          acc1 = mfma16(gt[0][1][s], h3[0][s], acc1);
-        }
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          acc0 = mfma16(gt[1][0][s], h3[1][s], acc0);
-          acc1 = mfma16(gt[1][1][s], h3[1][s], acc1);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          acc0[r] = (col_ok && hreal_d[0][r] && h3[0][r] > 0.f) ? acc0[r] : 0.f;
-          acc1[r] = (col_ok && hreal_d[1][r] && h3[1][r] > 0.f) ? acc1[r] : 0.f;
-        }
-        dh3[0] = acc0;
-        dh3[1] = acc1;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        sH1T[tw + r * S_T] = h1[0][r];
-        sH1T[tw + (16 + r) * S_T] = h1[1][r];
-        sZT[tw + r * S_T] = zb[r];
-      }
-#else
         {
           f32x4 acc0 = zero4(), acc1 = zero4();
           const f32x4 a00 = lds_read4(a4p);
@@ -1216,7 +907,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         }
       }
 #endif
-#endif  // FEDMX_HW_GRAM
       float prox_acc = 0.f;
       ++step;
 #pragma unroll

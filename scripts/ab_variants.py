@@ -17,14 +17,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from fedmse_decentralized_amd.ops import build  # noqa: E402
 
 VARIANTS = {
-    # r3: Gram-form step (FEDMX_HW_GRAM=1 default) against the round-2 helper-wave step
-    "gram0": ["-DFEDMX_HW_GRAM=0"],
-    "gram1": ["-DFEDMX_HW_GRAM=1"],
-    "gabl_k": ["-DFEDMX_HW_GRAM=1", "-DFEDMX_HW_ABLATE=128"],    # timing only: helpers skip the f64 Adam scalars
-    "gabl_tiles": ["-DFEDMX_HW_GRAM=1", "-DFEDMX_HW_ABLATE=256"],  # timing only: no G / W4^T X tiles
-    "gabl_l4": ["-DFEDMX_HW_GRAM=1", "-DFEDMX_HW_ABLATE=512"],     # timing only: no helper L4 / dW4 / Adam
-    "stamps_gram0": ["-DFEDMX_HW_GRAM=0", "-DFEDMX_STAMPS=1"],
-    "stamps_gram1": ["-DFEDMX_HW_GRAM=1", "-DFEDMX_STAMPS=1"],
+    # (r3 Gram-form step variants gram0/gram1/gabl_*/stamps_gram*: commit 6472e1c, profiles/r3_gram_form.md)
     # r3: helper-wave kernel step-loop fixes (scripts/gpu_train_ab.sh)
     "r0b0": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],   # round-2 code paths
     "r2b0": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],   # fenced dH3 reads only

@@ -56,21 +56,6 @@ PHASES_HW = [
     (12, 13, "epoch tail (barriers, validation, exchange, snapshot)"),
     (28, 29, "prologue (state load, mains)"), (30, 31, "epilogue (write back, mains)"),
 ]
-# Gram-form step (FEDMX_HW_GRAM=1, round 3): the helpers run layer 4, dY, dW4,
-# Adam and the next step's G / W4^T X partial sums
-PHASES_GRAM = [
-    (0, 1, "main: L1 partial write"), (1, 2, "main: barrier #1 wait"),
-    (2, 3, "main: L1 reduce + L2 + L3 + H3 publish"), (3, 4, "main: prefetch + W2/W3 reads"),
-    (4, 7, "main: barrier #2 wait"), (7, 8, "main: dH3 (G form) + dZ + dH1"),
-    (8, 9, "main: dW1 + small-tile MFMAs"), (9, 10, "main: adam W1"),
-    (10, 11, "main: next L1 + adam small + publish"), (0, 11, "main: STEP (stamp 0 -> 11)"),
-    (0, 2, "helper: barrier #1 wait"), (2, 6, "helper: scalars + reduce + prefetch"),
-    (6, 7, "helper: barrier #2 wait"), (7, 8, "helper: L4 + dY + loss"),
-    (8, 10, "helper: dW4 + adam W4"), (10, 11, "helper: publish W4 + G / W4^T X partials"),
-    (16, 17, "valid: one 16-row tile (one wave)"), (14, 15, "valid: epoch pass (per wave)"),
-    (12, 13, "epoch tail (barriers, validation, exchange, snapshot)"),
-    (28, 29, "prologue (state load, mains)"), (30, 31, "epilogue (write back, mains)"),
-]
 FOUR = "--four-waves" in sys.argv
 
 
@@ -88,7 +73,7 @@ def main():
     stamps = torch.zeros(8 * 32, dtype=torch.int64, device=dev)
     helper = not FOUR
     nw = 8 if helper else 4
-    phases = (PHASES_GRAM if "--gram" in sys.argv else PHASES_HW) if helper else PHASES4
+    phases = PHASES_HW if helper else PHASES4
     if PLAIN:
         for _ in range(3):
             _hip.train(eng.store, list(range(5)), hp, eng.dims, helper=helper)
