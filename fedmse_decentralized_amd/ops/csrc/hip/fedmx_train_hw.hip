@@ -36,49 +36,15 @@
 #ifndef FEDMX_HW_ABLATE
 #define FEDMX_HW_ABLATE 0
 #endif
-// dH3 partial reads: 0 = read-add per partial (the compiler serialised them
-// into six LDS round trips), 1 = all eight reads first, 2 = same + a
-// scheduling fence after the reads
-#ifndef FEDMX_HW_REDUCE
-#define FEDMX_HW_REDUCE 0
-#endif
-// 1: the helpers form step s+1's Adam scalars (an f64 dependency chain) in
-// their idle window between barriers #1 and #2 of step s instead of right
-// before barrier #1, where they sat on the helpers' path
-#ifndef FEDMX_HW_KEARLY
-#define FEDMX_HW_KEARLY 0
-#endif
-// 1: software-pipelined step tail (no FedProx): dW1 tiles in the order the
-// next chunk's layer 1 consumes them, each tile's Adam overlapping the next
-// tiles' MFMAs, the first layer-1 half overlapping the last tiles' Adam;
-// stages separated by scheduling fences.  Same per-element arithmetic and
-// summation order as the plain tail (bit-identical parameters).
-#ifndef FEDMX_HW_PIPE
-#define FEDMX_HW_PIPE 0
-#endif
 // 1: the Adam updates without FedProx in packed-fp32 form (adam4_packed)
 #ifndef FEDMX_HW_PACKED
 #define FEDMX_HW_PACKED 0
 #endif
-// bias column of X: 1 = the bias lanes load from kBiasX (address select),
-// 0 = overwrite the loaded registers (finalize)
-#ifndef FEDMX_HW_BIASX
-#define FEDMX_HW_BIASX 0
-#endif
-// issue priority of the main waves over their helpers (s_setprio level; 0: equal)
-// helpers sleep ~64 x N clocks after barrier #2 before their dW4 MFMAs (so
-// they do not contend for the matrix pipe with the mains' dZ / dH1 chain);
-// 0: no delay
-#ifndef FEDMX_HW_HDELAY
-#define FEDMX_HW_HDELAY 0
-#endif
-#ifndef FEDMX_HW_PRIO
-#define FEDMX_HW_PRIO 0
-#endif
-// issue priority of the helpers over their main waves (s_setprio level; 0: equal)
-#ifndef FEDMX_HW_HPRIO
-#define FEDMX_HW_HPRIO 0
-#endif
+// (Round 3 also measured, and removed, seven schedule variants of this step --
+// dH3 partial reads in flight together, the bias column by address select,
+// helper-formed next-step Adam scalars, a software-pipelined tail, helper
+// delays and issue priorities for either role: all slower or neutral,
+// profiles/r3_train_hw_experiments.md; source in git history before this note.)
 
 namespace fedmx {
 namespace hw {
@@ -180,10 +146,6 @@ struct XChunk {
   f32x4 f0, f1, b0, b1;
 };
 
-// what the bias lane reads for X's last four columns (padding, padding,
-// padding, the constant-1 bias column)
-__device__ __attribute__((aligned(16))) const float kBiasX[4] = {0.f, 0.f, 0.f, 1.f};
-
 template <bool PROX>
 __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   constexpr bool CP = true;
@@ -281,27 +243,24 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) brow_b[r] = batch_row_of_col<CP>(4 * g + r);
 
-  // The bias column DP-1 of X reads as 1 (it feeds W1a's b1 column): the
-  // lanes that hold it load from kBiasX instead of X.  Selecting the address
-  // (not overwriting the loaded register) leaves nothing that waits on the
-  // prefetch before its first real use: a post-load select was hoisted by the
-  // scheduler into the forward and stalled it on the prefetch every step.
+  // one batch chunk of X in both register layouts the step uses (f: layer
+  // 1's B operand over this wave's 32 columns; b: dW1's, batch on k);
+  // finalize_chunk then sets the bias column DP-1 to 1 (it feeds W1a's b1)
   auto load_chunk = [&](const float* X, int row0, int bc, XChunk& x) {
     const float* src = X + (size_t)(row0 + ((unsigned)brow_c < (unsigned)bc ? brow_c : 0)) * DP + xcol;
     x.f0 = *reinterpret_cast<const f32x4*>(src);
-    x.f1 = *reinterpret_cast<const f32x4*>(FEDMX_HW_BIASX && bias_lane ? kBiasX : src + 16);   // cols DP-4..DP-1
+    x.f1 = *reinterpret_cast<const f32x4*>(src + 16);   // cols 16.. of the block (DP-4..DP-1 on the bias lane)
     const float* bsrc = X + (size_t)row0 * DP + 32 * w + c;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {   // row quad 3 is padding, never read
       const int rr = ((unsigned)brow_b[r] < (unsigned)bc) ? brow_b[r] : 0;
       x.b0[r] = bsrc[(size_t)rr * DP];
-      x.b1[r] = *(FEDMX_HW_BIASX && bias_col ? kBiasX + 3 : bsrc + (size_t)rr * DP + 16);
+      x.b1[r] = bsrc[(size_t)rr * DP + 16];
     }
     x.b0[3] = 0.f;
     x.b1[3] = 0.f;
   };
-  auto finalize_chunk = [&](XChunk& x) {   // FEDMX_HW_BIASX == 0
-    if (FEDMX_HW_BIASX) return;
+  auto finalize_chunk = [&](XChunk& x) {
 #pragma unroll
     for (int r = 0; r < 3; ++r)
       if (bias_col) x.b1[r] = 1.f;
@@ -524,8 +483,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 
   if (helper) {
     // =========================== helper waves ===================================
-    if (FEDMX_HW_PRIO) __builtin_amdgcn_s_setprio(0);
-    if (FEDMX_HW_HPRIO) __builtin_amdgcn_s_setprio(FEDMX_HW_HPRIO);
     HSlab P4, M4, V4, AN4;
     stage_vals(pv_m);
     lds_to_hslab(M4, L);
@@ -558,7 +515,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         lds_write4(sK + 4 * (js & 1), f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f});
     };
     publish_k();   // step 0's
-    AdamStep KN = K;   // FEDMX_HW_KEARLY: the next step's scalars
     for (int ep = 0; ep < A.epochs; ++ep) {
       double acc_tr = 0.0;
       // W4 gradient + Adam between barrier #2 of step s and barrier #1 of s+1
@@ -567,31 +523,17 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         HSTAMP(hs, 0);
         __syncthreads();   // barrier #1 (main: layer-1 partials)
         HSTAMP(hs, 2);
-        if (FEDMX_HW_KEARLY) {
-          // step js+1's scalars into the other slot: the mains read slot js&1
-          // now and slot (js+1)&1 after barrier #1 of step js+1
-          const AdamStep Kcur = K;
-          next_constants();
-          KN = K;
-          K = Kcur;
-          if (lane == 0 && w8 == 4)
-            lds_write4(sK + 4 * ((js + 1) & 1), f32x4{KN.neg_step_size, KN.inv_bc2s, KN.bc2s, 0.f});
-        }
         __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
         HSTAMP(hs, 7);
         if (FEDMX_HW_ABLATE & 64) {
           ++js;
-          if (FEDMX_HW_KEARLY)
-            K = KN;
-          else
-            publish_k();
+          publish_k();
           continue;
         }
         const f32x4 w4a0 = lds_read4(sT0 + tr);
         const f32x4 w4a1 = lds_read4(sT0 + tr + 16 * S_T);
         const f32x4 w4b0 = lds_read4(sT1 + tr);
         const f32x4 w4b1 = lds_read4(sT1 + tr + 16 * S_T);
-        if (FEDMX_HW_HDELAY > 0) __builtin_amdgcn_s_sleep(FEDMX_HW_HDELAY);
         f32x4 G4[2][2];
 #pragma unroll
         for (int v = 0; v < 2; ++v)
@@ -626,10 +568,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         w4_to_lds(P4, L);
         publish_q4();
         ++js;
-        if (FEDMX_HW_KEARLY)
-          K = KN;
-        else
-          publish_k();   // step js's scalars, read by the mains after its barrier #1
+        publish_k();   // step js's scalars, read by the mains after its barrier #1
         HSTAMP(hs, 11);
       }
       double prox_now = 0.0;
@@ -662,8 +601,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 
   // ============================= main waves =====================================
   int js = 0;   // step index within the launch (selects the Adam-scalar slot)
-  // (FEDMX_HW_PRIO: the chain's wave wins issue arbitration against its helper)
-  if (FEDMX_HW_PRIO) __builtin_amdgcn_s_setprio(FEDMX_HW_PRIO);
   MSlab P, M, V, AN;
   stage_vals(pv_m);
   lds_to_mslab(M, L);
@@ -870,7 +807,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       __syncthreads();  // barrier #2: dH3 partials of all waves visible
       HSTAMP(ms, 7);
       f32x4 dh3[2];
-#if FEDMX_HW_REDUCE == 0
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         f32x4 s = lds_read4(sRedDH3 + t * 256 + lane * 4);
@@ -884,29 +820,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         for (int r = 0; r < 4; ++r) s[r] = (hreal_d[t][r] && h3[t][r] > 0.f) ? s[r] : 0.f;
         dh3[t] = s;
       }
-#else
-      {
-        // all eight partial reads in flight before the first add (one LDS
-        // round trip; the compiler otherwise serialised them into six)
-        f32x4 pr[2][4];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int ww = 0; ww < 4; ++ww) pr[t][ww] = lds_read4(sRedDH3 + (ww * 2 + t) * 256 + lane * 4);
-        if (FEDMX_HW_REDUCE == 2) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          f32x4 s = pr[t][0];
-#pragma unroll
-          for (int ww = 1; ww < 4; ++ww)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s[r] = s[r] + pr[t][ww][r];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) s[r] = (hreal_d[t][r] && h3[t][r] > 0.f) ? s[r] : 0.f;
-          dh3[t] = s;
-        }
-      }
-#endif
       float prox_acc = 0.f;
       ++step;
 #pragma unroll
@@ -935,58 +848,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         dh1b[t] = acc;
       }
       HSTAMP(ms, 8);
-#if FEDMX_HW_PIPE   // 1: fenced stages, 2: source order only
-      if (!PROX) {
-        // ---- stage A: the two dW1 tiles the next layer-1 f0 half waits for
-#pragma unroll
-        for (int s = 0; s < KB; ++s) {
-          G1[0][0] = mfma16(cur.b0[s], dh1b[0][s], G1[0][0]);
-          G1[1][0] = mfma16(cur.b0[s], dh1b[1][s], G1[1][0]);
-        }
-        wave_sync();
-        if (FEDMX_HW_PIPE == 1) __builtin_amdgcn_sched_barrier(0);
-        // ---- stage B: the other two tiles + the small tile || Adam of (0,0), (1,0)
-        const f32x4 sa = lds_read4(w < 2 ? sT2 + tr + 16 * w * S_T : sDZT + tr);
-        const f32x4 sbz = lds_read4(sZT + tr);
-        const f32x4 sb = (w < 2) ? sbz : ((w == 2) ? h1b[0] : h1b[1]);
-#pragma unroll
-        for (int s = 0; s < KB; ++s) {
-          G1[0][1] = mfma16(cur.b1[s], dh1b[0][s], G1[0][1]);
-          G1[1][1] = mfma16(cur.b1[s], dh1b[1][s], G1[1][1]);
-        }
-#pragma unroll
-        for (int s = 0; s < KB; ++s) Go = mfma16(sa[s], sb[s], Go);
-        float pacc = 0.f;
-        adam4<false>(P.q1[0][0], M.q1[0][0], V.q1[0][0], AN.q1[0][0], G1[0][0], K, pacc);
-        adam4<false>(P.q1[1][0], M.q1[1][0], V.q1[1][0], AN.q1[1][0], G1[1][0], K, pacc);
-        HSTAMP(ms, 9);
-        if (FEDMX_HW_PIPE == 1) __builtin_amdgcn_sched_barrier(0);
-        // ---- stage C: next layer-1 f0 half || Adam of (0,1), (1,1)
-        f32x4 acc0 = zero4(), acc1 = zero4();
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc0 = mfma16(P.q1[0][0][j], nxt.f0[j], acc0);
-          acc1 = mfma16(P.q1[1][0][j], nxt.f0[j], acc1);
-        }
-        adam4<false>(P.q1[0][1], M.q1[0][1], V.q1[0][1], AN.q1[0][1], G1[0][1], K, pacc);
-        adam4<false>(P.q1[1][1], M.q1[1][1], V.q1[1][1], AN.q1[1][1], G1[1][1], K, pacc);
-        HSTAMP(ms, 10);
-        if (FEDMX_HW_PIPE == 1) __builtin_amdgcn_sched_barrier(0);
-        // ---- stage D: next layer-1 f1 half || small-tile Adam, publish
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc0 = mfma16(P.q1[0][1][j], nxt.f1[j], acc0);
-          acc1 = mfma16(P.q1[1][1][j], nxt.f1[j], acc1);
-        }
-        l1a = acc0;
-        l1b = acc1;
-        adam4<false>(P.o, M.o, V.o, AN.o, Go, K, pacc);
-        own_to_lds(P, L);   // read by every wave after barrier #1
-        HSTAMP(ms, 11);
-        cur = nxt;
-        continue;
-      }
-#endif
       // ---- dW1^T (own columns) = X^T dH1
 #pragma unroll
       for (int s = 0; s < KB; ++s) {

@@ -18,29 +18,15 @@ from fedmse_decentralized_amd.ops import build  # noqa: E402
 
 VARIANTS = {
     # (r3 Gram-form step variants gram0/gram1/gabl_*/stamps_gram*: commit 6472e1c, profiles/r3_gram_form.md)
-    # r3: helper-wave kernel step-loop fixes (scripts/gpu_train_ab.sh)
-    "r0b0": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],   # round-2 code paths
-    "r2b0": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],   # fenced dH3 reads only
-    "r0b1": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],   # bias-column address select only
-    "r1b1": ["-DFEDMX_HW_REDUCE=1", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],   # unfenced grouped reads + select
-    "r2b1": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],   # both
-    "r0b0k": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=1", "-DFEDMX_HW_PIPE=0"],  # early Adam scalars only
-    "r2b1k": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=1", "-DFEDMX_HW_PIPE=0"],  # three
-    "r0b0p": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=1"],  # pipelined tail only
-    "r1b0": ["-DFEDMX_HW_REDUCE=1", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=0"],  # grouped reads, unfenced
-    "r0b0q": ["-DFEDMX_HW_REDUCE=0", "-DFEDMX_HW_BIASX=0", "-DFEDMX_HW_KEARLY=0", "-DFEDMX_HW_PIPE=2"],  # tail in pipeline order, unfenced
-    # r3: helper-side timing probes (train launch us, base 945 / 947 on the same box)
-    "hd8": ["-DFEDMX_HW_HDELAY=8"],                  # helpers wait ~512 clocks before dW4   1049 (+11 %)
-    "hd16": ["-DFEDMX_HW_HDELAY=16"],                # ~1 K clocks                           1064
-    "hd24": ["-DFEDMX_HW_HDELAY=24"],                # ~1.5 K clocks                         1088
-    "hprio1": ["-DFEDMX_HW_HPRIO=1"],                # helpers at issue priority 1 over the mains   1071 (+13 %)
-    "hprio3": ["-DFEDMX_HW_HPRIO=3"],                # helpers at issue priority 3                  1070
+    # r3: helper-wave kernel step-loop variants r0b0 r2b0 r0b1 r1b1 r2b1 r0b0k r2b1k r0b0p r1b0 r0b0q,
+    # helper delays hd8/16/24, priorities hprio1/3 and (r2) hwprio1/3: all measured slower or
+    # neutral (profiles/r3_train_hw_experiments.md); their switches were removed from the kernel
+    # (source in git history, commit 5365856)
     "packed": ["-DFEDMX_HW_PACKED=1"],               # packed-fp32 Adam (bit-identical)  966-974 vs 948-951 (+2 %)
     "abl_pf": ["-DFEDMX_HW_ABLATE=8"],               # timing only: prefetch always hits the cache
     "abl_hadam": ["-DFEDMX_HW_ABLATE=16"],           # timing only: helpers skip W4's Adam
     "abl_madam": ["-DFEDMX_HW_ABLATE=32"],           # timing only: mains skip W1's Adam
     "abl_hnone": ["-DFEDMX_HW_ABLATE=64"],           # timing only: helpers idle between barriers
-    "r2b1kp": ["-DFEDMX_HW_REDUCE=2", "-DFEDMX_HW_BIASX=1", "-DFEDMX_HW_KEARLY=1", "-DFEDMX_HW_PIPE=1"],  # all four
     "base": [],                                   # defaults: compact order, FMA Adam, iglp_opt(0), VGPR-form MFMA
     "sched0": ["-DFEDMX_SCHED_HINTS=0"],          # compiler schedule          (+2.5%, measured)
     "hint1": ["-DFEDMX_SCHED_HINTS=1"],           # 64 x (1 MFMA, 6 VALU)      (+9%)
@@ -52,8 +38,6 @@ VARIANTS = {
     "w4pos1": ["-DFEDMX_W4_POS=1"],               # W4 Adam after dH1, fenced   (+2.5%)
     "w4pos2": ["-DFEDMX_W4_POS=2"],               # W4 Adam after the next L1 issue, fenced (+2%)
     "nohw": ["-DFEDMX_TRAIN_HW_DEFAULT=0"],       # 4-wave kernel for the compact shapes too (+3%, FedProx +8%)
-    "hwprio1": ["-DFEDMX_HW_PRIO=1"],             # main waves at issue priority 1 over helpers (+0.4%)
-    "hwprio3": ["-DFEDMX_HW_PRIO=3"],             # main waves at issue priority 3 (+0.4%)
     "scaled": ["-DFEDMX_ADAM_SCALED=1"],          # scaled-moment Adam, 5 VALU/param (+0.5%)
     # helper-wave kernel, timing-only ablations of the main waves' step (r2, base
     # 1.059 ms; per-step Adam constants on the mains: 0.992 ms without -> moved
