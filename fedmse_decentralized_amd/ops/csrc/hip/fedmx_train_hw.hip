@@ -632,6 +632,15 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     }
   };
 
+  // the step's 1/bt and dY scale 2/(bt d_in): bt is B except on an epoch's
+  // last batch, so both are formed once here (IEEE divisions, the same values
+  // as per step) instead of two division sequences in every step
+  const int bt_last = nb > 0 ? n_tr - (nb - 1) * B : B;
+  float inv_b_full = 1.0f / (float)B, inv_b_last = 1.0f / (float)bt_last;
+  float scale_full = 2.0f / (float)(B * d_in), scale_last = 2.0f / (float)(bt_last * d_in);
+  // opaque to the optimiser: it would otherwise fold the per-step select of
+  // two quotients back into one division of the selected divisor
+  asm volatile("" : "+v"(inv_b_full), "+v"(inv_b_last), "+v"(scale_full), "+v"(scale_last));
   for (int ep = 0; ep < A.epochs; ++ep) {
     double acc_tr = 0.0;
     XChunk cur, nxt;
@@ -647,7 +656,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       const bool has_next = bi + 1 < nb;
       const int row_n = (bi + 1) * B;
       const int bc_n = has_next ? min(B, n_tr - row_n) : 0;
-      const float inv_bt = 1.0f / (float)bt;
+      const float inv_bt = has_next ? inv_b_full : inv_b_last;
       const bool ms = (ep == 0 && bi == STAMP_STEP);
       HSTAMP(ms, 0);
       f32x4 G1[2][2], Go = zero4();
@@ -773,7 +782,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 
       // ---- dY (masked, feature-major); dY^T / H3^T for the helper's dW4
       const bool col_ok = (unsigned)brow_c < (unsigned)bt;
-      const float scale = col_ok ? 2.0f / (float)(bt * d_in) : 0.f;
+      const float scale = col_ok ? (has_next ? scale_full : scale_last) : 0.f;
       f32x4 dy[2];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
