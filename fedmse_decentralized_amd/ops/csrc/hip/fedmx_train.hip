@@ -623,6 +623,14 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   double min_valid = __builtin_huge_val();
   int worse = 0, ep_run = 0, best_ep = -1;
 
+  // the step's 1/bt and dY scale 2/(bt d_in): bt is B except on an epoch's
+  // last batch, so both are formed once here instead of two IEEE division
+  // sequences per chunk (opaque to LLVM, which would otherwise fold the
+  // per-chunk select back into one division of the selected divisor)
+  const int bt_last = nb > 0 ? n_tr - (nb - 1) * B : B;
+  float inv_b_full = 1.0f / (float)B, inv_b_last = 1.0f / (float)bt_last;
+  float scale_full = 2.0f / (float)(B * d_in), scale_last = 2.0f / (float)(bt_last * d_in);
+  asm volatile("" : "+v"(inv_b_full), "+v"(inv_b_last), "+v"(scale_full), "+v"(scale_last));
   for (int ep = 0; ep < A.epochs; ++ep) {
     double acc_tr = 0.0;
     // The epoch is a sequence of chunks (batch bi, column tile ch).  The next
@@ -651,7 +659,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       const bool has_next = bi_n < nb;
       const int row_n = bi_n * B + 16 * ch_n;
       const int bc_n = has_next ? min(16, min(B, n_tr - bi_n * B) - 16 * ch_n) : 0;
-      const float inv_bt = 1.0f / (float)bt;
+      const bool full_b = bi + 1 < nb;
+      const float inv_bt = full_b ? inv_b_full : inv_b_last;
       if (ch == 0) {
         // bias corrections of the Adam step this batch closes (python:
         // 1 - beta ** step), computed at the batch start, off the critical path
@@ -696,7 +705,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
 
       // ---- dY (masked, feature-major) and the transposes feeding dW4
       const bool col_ok = (unsigned)brow_c < (unsigned)bc;
-      const float scale = col_ok ? 2.0f / (float)(bt * d_in) : 0.f;
+      const float scale = col_ok ? (full_b ? scale_full : scale_last) : 0.f;
       f32x4 dy[2];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
