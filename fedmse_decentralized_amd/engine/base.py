@@ -100,17 +100,23 @@ class ClientStore:
         self.test_label = None
 
     @staticmethod
-    def _concat(arrays: Sequence[np.ndarray], device):
+    def _concat(arrays: Sequence[np.ndarray], device, bias_column: bool = False):
         offs = np.zeros(len(arrays) + 1, dtype=np.int64)
         for i, a in enumerate(arrays):
             offs[i + 1] = offs[i] + a.shape[0]
         buf = np.concatenate([pad_features(a) for a in arrays], 0) if arrays else np.zeros((0, DP), np.float32)
+        if bias_column:
+            # the training kernels read X's padded column DP-1 as the constant 1
+            # that feeds W1a's bias column: stored, so the helper-wave kernel
+            # need not overwrite it after every batch load.  Every other reader
+            # ignores the column (forward SSEs sum d < d_in, the oracle slices).
+            buf[:, DP - 1] = 1.0
         return torch.from_numpy(buf).to(device), offs
 
     def load_data(self, train: Sequence[np.ndarray], valid: Sequence[np.ndarray],
                   test: Sequence[np.ndarray], test_label: Sequence[np.ndarray]):
-        self.train, self.train_off = self._concat(train, self.device)
-        self.valid, self.valid_off = self._concat(valid, self.device)
+        self.train, self.train_off = self._concat(train, self.device, bias_column=True)
+        self.valid, self.valid_off = self._concat(valid, self.device, bias_column=True)
         self.test, self.test_off = self._concat(test, self.device)
         lab = np.concatenate([np.asarray(l, dtype=np.int32) for l in test_label]) if test_label else np.zeros(0, np.int32)
         self.test_label = torch.from_numpy(lab).to(self.device)

@@ -36,6 +36,12 @@
 #ifndef FEDMX_HW_ABLATE
 #define FEDMX_HW_ABLATE 0
 #endif
+// 1: X's bias column DP-1 is read from memory (the packed training /
+// validation rows store the constant 1 there) instead of being set after each
+// load
+#ifndef FEDMX_HW_XBIAS
+#define FEDMX_HW_XBIAS 1
+#endif
 // 1: the Adam updates without FedProx in packed-fp32 form (adam4_packed)
 #ifndef FEDMX_HW_PACKED
 #define FEDMX_HW_PACKED 0
@@ -260,7 +266,10 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     x.b0[3] = 0.f;
     x.b1[3] = 0.f;
   };
+  // (FEDMX_HW_XBIAS: the packed rows already hold the 1 in column DP-1,
+  // ClientStore._concat -- nothing to overwrite after the load)
   auto finalize_chunk = [&](XChunk& x) {
+    if (FEDMX_HW_XBIAS) return;
 #pragma unroll
     for (int r = 0; r < 3; ++r)
       if (bias_col) x.b1[r] = 1.f;
@@ -291,7 +300,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) xf[b][v][r] = q[r];
       }
-    if (g == 3) xf[3][1][3] = 1.f;
+    if (!FEDMX_HW_XBIAS && g == 3) xf[3][1][3] = 1.f;
     f32x4 h1[2];
     {
       f32x4 sum0 = zero4(), sum1 = zero4();
