@@ -99,12 +99,18 @@ class ClientStore:
         self.train_off = self.valid_off = self.test_off = None
         self.test_label = None
 
+    # zero rows after the last client's training rows: the helper-wave
+    # kernel's batch loads (batch <= 12) read whole 12-row chunks without
+    # clamping rows past a client's end (those columns are masked)
+    TRAIN_TAIL_ROWS = 16
+
     @staticmethod
-    def _concat(arrays: Sequence[np.ndarray], device, bias_column: bool = False):
+    def _concat(arrays: Sequence[np.ndarray], device, bias_column: bool = False, tail_rows: int = 0):
         offs = np.zeros(len(arrays) + 1, dtype=np.int64)
         for i, a in enumerate(arrays):
             offs[i + 1] = offs[i] + a.shape[0]
-        buf = np.concatenate([pad_features(a) for a in arrays], 0) if arrays else np.zeros((0, DP), np.float32)
+        parts = [pad_features(a) for a in arrays] + [np.zeros((tail_rows, DP), np.float32)]
+        buf = np.concatenate(parts, 0)
         if bias_column:
             # the training kernels read X's padded column DP-1 as the constant 1
             # that feeds W1a's bias column: stored, so the helper-wave kernel
@@ -115,7 +121,8 @@ class ClientStore:
 
     def load_data(self, train: Sequence[np.ndarray], valid: Sequence[np.ndarray],
                   test: Sequence[np.ndarray], test_label: Sequence[np.ndarray]):
-        self.train, self.train_off = self._concat(train, self.device, bias_column=True)
+        self.train, self.train_off = self._concat(train, self.device, bias_column=True,
+                                                  tail_rows=self.TRAIN_TAIL_ROWS)
         self.valid, self.valid_off = self._concat(valid, self.device, bias_column=True)
         self.test, self.test_off = self._concat(test, self.device)
         lab = np.concatenate([np.asarray(l, dtype=np.int32) for l in test_label]) if test_label else np.zeros(0, np.int32)

@@ -252,16 +252,24 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // one batch chunk of X in both register layouts the step uses (f: layer
   // 1's B operand over this wave's 32 columns; b: dW1's, batch on k);
   // finalize_chunk then sets the bias column DP-1 to 1 (it feeds W1a's b1)
+  // Rows past the client's end (an epoch's last chunk) are read as they are:
+  // the next client's rows or the buffer's zero tail (ClientStore), finite
+  // values in batch columns every product masks.  So each load is a uniform
+  // row base plus a per-lane offset formed once, with no per-step clamping.
+  // (padding columns, brow_c = -1, read the chunk's row 0; every row < 12)
+  const unsigned offf = (unsigned)((brow_c < 0 ? 0 : brow_c) * DP + xcol);
+  unsigned offb[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) offb[r] = (unsigned)(brow_b[r] * DP + 32 * w + c);   // r < 3: real rows
   auto load_chunk = [&](const float* X, int row0, int bc, XChunk& x) {
-    const float* src = X + (size_t)(row0 + ((unsigned)brow_c < (unsigned)bc ? brow_c : 0)) * DP + xcol;
-    x.f0 = *reinterpret_cast<const f32x4*>(src);
-    x.f1 = *reinterpret_cast<const f32x4*>(src + 16);   // cols 16.. of the block (DP-4..DP-1 on the bias lane)
-    const float* bsrc = X + (size_t)row0 * DP + 32 * w + c;
+    (void)bc;
+    const float* base = X + (size_t)row0 * DP;
+    x.f0 = *reinterpret_cast<const f32x4*>(base + offf);
+    x.f1 = *reinterpret_cast<const f32x4*>(base + offf + 16);   // cols DP-4..DP-1 on the bias lane
 #pragma unroll
     for (int r = 0; r < 3; ++r) {   // row quad 3 is padding, never read
-      const int rr = ((unsigned)brow_b[r] < (unsigned)bc) ? brow_b[r] : 0;
-      x.b0[r] = bsrc[(size_t)rr * DP];
-      x.b1[r] = bsrc[(size_t)rr * DP + 16];
+      x.b0[r] = base[offb[r]];
+      x.b1[r] = base[offb[r] + 16];
     }
     x.b0[3] = 0.f;
     x.b1[3] = 0.f;
