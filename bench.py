@@ -9,13 +9,25 @@ validation every epoch), MSE-scored aggregator election, FedMSE aggregation
 SAE-CEN evaluation (ROC-AUC) of every client, results/verification JSONL and
 per-client model.cpt / training_tracking.pkl artefacts.
 
-Scaling (weak): every GPU hosts 10 clients (one process per GPU); N GPUs run
-ONE decentralised federation of 10*N clients (the reference's 10/15/20/50-client
-network-scale configs generalised), with the vote scores, FedMSE weights and
-AUCs exchanged by RCCL all-reduce and the selected models by an RCCL
-all-gather over xGMI.  ``value`` is the whole-job throughput expressed in
-10-client-federation rounds per second: (rounds/s of the federation) x
-(clients / 10); at N=1 it is exactly the 10-client federation's rounds/s.
+Multi-GPU (N > 1, one process per GPU).  ``value`` is ALWAYS the
+10-client federation's rounds/s, the BASELINE metric's named configuration:
+at N > 1 its 10 clients are sharded over the N ranks (BASELINE config 4's
+shape; strong scaling), with vote scores, FedMSE weights and AUCs exchanged
+by RCCL all-reduce and the selected models by an RCCL all-gather over xGMI.
+No x N factor is applied: five trained clients occupy 5 of one GPU's 256 CUs,
+so sharding them can only add exchange latency, and the curve shows that.
+Two further measurements ride along in their own fields, never folded into
+``value``:
+  * ``weak_scaling`` – ONE decentralised federation of 10*N clients (10 per
+    GPU; the reference's 10/15/20/50-client network-scale configs
+    generalised): its rounds/s and AUC;
+  * ``independent_federations`` – N concurrent one-GPU 10-client federations,
+    one per rank with its own seed, no collectives (experiment-level
+    parallelism: the reference's runs loop, `src/main.py:108-110`): the
+    aggregate rounds/s of the job.
+``--clients C`` / ``--clients-per-gpu K`` choose another headline federation
+(C clients, or K*N clients) — e.g. ``--clients-per-gpu 1`` is BASELINE
+config 3 (8 clients, one per GPU).
 
 Data: synthetic N-BaIoT-shaped tabular data (115 features, per-client sizes of
 the shipped IID-10 split) with random-init weights of the reference
@@ -35,14 +47,20 @@ import sys
 import tempfile
 import time
 
-from fedmse_decentralized_amd.io.files import reserve_fd_table
+from fedmse_decentralized_amd.parallel.env import export_comm_env
+
+# RCCL's transport settings reach HSA only if exported before the HIP runtime
+# starts (parallel/env.py): first statement, before torch is imported
+export_comm_env()
+
+from fedmse_decentralized_amd.io.files import reserve_fd_table  # noqa: E402
 
 # grow the descriptor table while the process is still single-threaded
 # (io.files.reserve_fd_table: later growth waits on RCU in threaded processes)
 reserve_fd_table()
 
-import numpy as np
-import torch
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 BASELINE_ROUNDS_PER_SEC = 0.30
 METRIC = "rounds/sec + detection AUC, 10-client SAE (N-BaIoT shape) at 1/2/4/8 MI355X"
@@ -87,8 +105,7 @@ def _spawn_ranks(n: int, argv) -> int:
         port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env = dict(os.environ)   # carries COMM_ENV (exported at import)
     return subprocess.run(cmd, env=env).returncode
 
 
@@ -183,15 +200,27 @@ def _measure(fed, comm, device, steps: int, warmup: int, profile):
     return dt, last, train_ms, epochs_mean
 
 
+def _auc(last, fed=None, phantom=False):
+    """(mean, min) detection AUC over the federation's clients after the last
+    timed round.  A phantom rank only ever evaluates its own clients (the AUC
+    all-reduce is stubbed): those, not the zero-filled others."""
+    if last is None:
+        return float("nan"), float("nan")
+    m = np.asarray(last.metrics, dtype=np.float64)
+    if phantom and fed is not None and fed.local:
+        m = m[fed.local[0]:fed.local[-1] + 1]
+    return float(np.mean(m)), float(np.min(m))
+
+
 def _main(argv, real_stdout: int):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--clients-per-gpu", type=int, default=10)
     p.add_argument("--clients", type=int, default=None,
-                   help="fixed federation size (strong scaling, e.g. the paper's 10 clients on 8 GPUs); "
-                        "default: clients-per-gpu x GPUs (weak scaling)")
+                   help="headline federation size (default 10: BASELINE's 10-client federation at every N)")
+    p.add_argument("--clients-per-gpu", type=int, default=None,
+                   help="headline = ONE federation of K x N clients (weak scaling; K=1 is BASELINE config 3)")
     p.add_argument("--lr", type=float, default=1e-3)
     p.add_argument("--shrink-lambda", type=float, default=5.0)
     p.add_argument("--epochs", type=int, default=5)
@@ -213,19 +242,23 @@ def _main(argv, real_stdout: int):
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
     p.add_argument("--profile", default=None, help="cProfile the timed rounds (rank 0) into this file")
     p.add_argument("--phantom-ranks", type=int, default=0,
-                   help="projection on ONE GPU: run rank 0 of a W-rank weak-scaling job with the collectives "
-                        "stubbed out (parallel.comm.PhantomComm); the record is labelled as a projection")
-    p.add_argument("--no-strong", action="store_true",
-                   help="N > 1: skip the extra strong-scaling run of the 10-client federation over the N ranks")
+                   help="projection on ONE GPU: run rank 0 of a W-rank weak-scaling job (10 clients per rank) "
+                        "with the collectives stubbed out (parallel.comm.PhantomComm); labelled as a projection")
+    p.add_argument("--no-extra", action="store_true",
+                   help="N > 1: skip the weak_scaling and independent_federations measurements")
     args = p.parse_args(argv)
+    if args.clients is not None and args.clients_per_gpu is not None:
+        p.error("--clients and --clients-per-gpu are exclusive")
 
     from fedmse_decentralized_amd.config import ExperimentConfig
     from fedmse_decentralized_amd.federation import Federation
+    from fedmse_decentralized_amd.parallel.comm import LoopbackComm
     from fedmse_decentralized_amd.parallel.launch import init_comm, shutdown
     from fedmse_decentralized_amd.utils.logging import setup_logging
 
     device = "cuda" if torch.cuda.is_available() else "cpu"
-    if args.phantom_ranks > 1:
+    phantom = args.phantom_ranks > 1
+    if phantom:
         from fedmse_decentralized_amd.parallel.comm import PhantomComm
 
         comm = PhantomComm(args.phantom_ranks, device)
@@ -236,24 +269,32 @@ def _main(argv, real_stdout: int):
     if args.gpus != n_gpus and comm.is_root:
         print(f"note: --gpus {args.gpus} but world size is {n_gpus}; using the world size", file=sys.stderr)
     out_root = tempfile.mkdtemp(prefix="fedmx_bench_") if comm.is_root else tempfile.mkdtemp(prefix="fedmx_bench_r")
-    phantom = args.phantom_ranks > 1
 
-    def build(network_size: int):
+    def build(network_size: int, fcomm=comm, run: int = 0):
         cfg = ExperimentConfig(
             num_participants=0.5, epoch=args.epochs, num_rounds=10 ** 9, lr_rate=args.lr,
             shrink_lambda=args.shrink_lambda, network_size=network_size, batch_size=args.batch_size,
             model_types=[args.model_type], update_types=[args.update_type],
             synthetic=args.data_kind, synthetic_iid=not args.non_iid, compat=args.compat, backend=args.backend,
-            global_early_stop=False, save_checkpoints=not args.no_artifacts, output_root=out_root,
+            global_early_stop=False, save_checkpoints=not args.no_artifacts,
+            output_root=os.path.join(out_root, f"fed{network_size}_run{run}"),
             trace_file=args.trace, log_level="WARNING", init_mode=args.init_mode)
-        fed = Federation(cfg, args.model_type, args.update_type, run=0, comm=comm,
+        fed = Federation(cfg, args.model_type, args.update_type, run=run, comm=fcomm,
                          write_reports=not args.no_artifacts).setup()
         if phantom and fed._fast is None:
             # the host protocol reads other ranks' vote records, which a phantom job does not have
             raise SystemExit("--phantom-ranks needs the device-resident round protocol (HIP engine, compat fixed)")
         return fed
 
-    fed = build(args.clients if args.clients else args.clients_per_gpu * n_gpus)
+    # the headline federation: BASELINE's 10 clients unless asked otherwise;
+    # a phantom projection is of the weak-scaling job (10 clients per rank)
+    if phantom:
+        clients, scaling = 10 * args.phantom_ranks, "weak"
+    elif args.clients_per_gpu is not None:
+        clients, scaling = args.clients_per_gpu * n_gpus, "weak"
+    else:
+        clients, scaling = (args.clients or 10), "strong"
+    fed = build(clients)
     # N > 1: time every rank's training launch (HIP events around it), so the
     # cost of waiting for the slowest rank's largest client is measured
     time_train = n_gpus > 1 and fed._fast is not None
@@ -261,44 +302,27 @@ def _main(argv, real_stdout: int):
         fed._fast.train_timing = True
     dt, last, train_ms, epochs_mean = _measure(fed, comm, device, args.steps, args.warmup, args.profile)
     fed_rps = args.steps / dt
-    # whole-job value: with the default 10 clients per GPU the federation has
-    # 10*N clients and the job does N 10-client federations' worth of work
-    # per round; for a fixed federation size (--clients) the round rate itself
-    world_for_value = args.phantom_ranks if phantom else n_gpus
-    per_gpu_default = args.clients is None and args.clients_per_gpu == 10
-    value = fed_rps * world_for_value if per_gpu_default else fed_rps
-    if last is not None:
-        # a phantom rank only ever evaluates its own clients (the AUC
-        # all-reduce is stubbed): report those, not the zero-filled others
-        m = np.asarray(last.metrics, dtype=np.float64)
-        if phantom and fed.local:
-            m = m[fed.local[0]:fed.local[-1] + 1]
-        auc, auc_min = float(np.mean(m)), float(np.min(m))
-    else:
-        auc = auc_min = float("nan")
+    auc, auc_min = _auc(last, fed, phantom)
     rec = None
     if comm.is_root:
-        unit = ("10-client-federation rounds/s, whole job (= federation rounds/s x clients / 10)" if per_gpu_default
-                else "federation rounds/s")
         rec = {
             "metric": METRIC,
-            "value": None if phantom else round(value, 4),
-            "unit": unit,
+            "value": None if phantom else round(fed_rps, 4),
+            "unit": f"rounds/s of one {fed.N}-client federation (whole job, all {n_gpus} GPU(s))",
             "n_gpus": 1 if phantom else n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * dt / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "strong" if args.clients else "weak",
-            "vs_baseline": None if phantom else round(value / BASELINE_ROUNDS_PER_SEC, 2),
+            "scaling": scaling,
+            "vs_baseline": None if phantom else round(fed_rps / BASELINE_ROUNDS_PER_SEC, 2),
             "dtype": "fp32",
             "data": (f"synthetic ({'N-BaIoT' if args.data_kind == 'nbaiot' else 'Kitsune'}-shaped, 115 features, "
                      f"{'non-IID (Dirichlet)' if args.non_iid else 'IID'} client mixtures, "
                      f"{'IID-10 client sizes' if not args.non_iid else 'Dirichlet client sizes'}); "
                      "random-init weights"),
             "config": {
-                "model": f"SAE 115-27-7-27-115 ({args.model_type}, {args.update_type}), "
-                         + (f"{args.clients} clients" if args.clients else f"{args.clients_per_gpu} clients/GPU"),
+                "model": f"SAE 115-27-7-27-115 ({args.model_type}, {args.update_type}), {fed.N} clients",
                 "global_batch": args.batch_size,
                 "seq_len": 115,
                 "parallelism": f"client-sharded x{n_gpus} ({_collectives_label(comm)})",
@@ -307,6 +331,8 @@ def _main(argv, real_stdout: int):
                 "local_epochs": args.epochs,
                 "backend": fed.engine.name,
                 "compat": args.compat,
+                # the shared initial model (compat fixed default since r3) changes
+                # AUC and epochs run vs per_client records: compare like with like
                 "init_mode": fed.cfg.resolved_init_mode(),
                 "device_protocol": fed._fast is not None,
             },
@@ -334,24 +360,46 @@ def _main(argv, real_stdout: int):
             # a one-GPU projection, not a multi-GPU measurement: n_gpus stays 1
             # and the whole-job figure goes to projected_value
             rec["projected_ranks"] = args.phantom_ranks
-            rec["projected_value"] = round(value, 4)
+            rec["projected_value"] = round(fed_rps, 4)
             rec["detection_auc_scope"] = "rank-0 clients only"
             rec["projection"] = (f"rank 0 of a {args.phantom_ranks}-rank job on ONE GPU, collectives stubbed "
                                  "(no RCCL time); projected_value assumes every rank is as fast as this one")
-    if n_gpus > 1 and not phantom and args.clients is None and not args.no_strong:
-        # the same 10-client federation the 1-GPU run measures, now spread over
-        # the N ranks (strong scaling, BASELINE config 4's shape): reported
-        # beside the weak-scaling headline, not folded into it
+    if n_gpus > 1 and not phantom and not args.no_extra:
         fed.finish()
-        fed10 = build(10)
-        dt10, last10, _, _ = _measure(fed10, comm, device, args.steps, args.warmup, None)
+        # (a) weak scaling: one federation of 10 clients per GPU
+        if fed.N != 10 * n_gpus:
+            fw = build(10 * n_gpus)
+            dtw, lastw, _, _ = _measure(fw, comm, device, args.steps, args.warmup, None)
+            aw, aw_min = _auc(lastw)
+            fw.finish()
+            del fw
+        else:
+            dtw, aw, aw_min = dt, auc, auc_min
+        # (b) experiment-level parallelism: every rank its own one-GPU 10-client
+        # federation (run index = rank, i.e. its own seeds), no collectives;
+        # the job's clock is the slowest rank's, as for the headline
+        fi = build(10, fcomm=LoopbackComm(comm.device), run=comm.rank)
+        dti, lasti, _, _ = _measure(fi, comm, device, args.steps, args.warmup, None)
+        ai = comm.all_gather(torch.tensor(_auc(lasti), dtype=torch.float64)).reshape(n_gpus, 2).numpy()
+        fi.finish()
         if rec is not None:
-            m10 = np.asarray(last10.metrics, dtype=np.float64)
-            rec["strong_scaling_10_clients"] = {
-                "federation_rounds_per_sec": round(args.steps / dt10, 4),
-                "ms_per_step": round(1e3 * dt10 / args.steps, 4),
-                "detection_auc_mean": round(float(m10.mean()), 6),
-                "detection_auc_min": round(float(m10.min()), 6)}
+            rec["weak_scaling"] = {
+                "clients": 10 * n_gpus,
+                "federation_rounds_per_sec": round(args.steps / dtw, 4),
+                "ms_per_step": round(1e3 * dtw / args.steps, 4),
+                "detection_auc_mean": round(aw, 6),
+                "detection_auc_min": round(aw_min, 6),
+                "note": "ONE federation of 10 clients per GPU; rounds/s of that larger federation (not x N)"}
+            rec["independent_federations"] = {
+                "federations": n_gpus,
+                "clients_each": 10,
+                "aggregate_rounds_per_sec": round(n_gpus * args.steps / dti, 4),
+                "per_federation_rounds_per_sec": round(args.steps / dti, 4),
+                "ms_per_step": round(1e3 * dti / args.steps, 4),
+                "detection_auc_mean": round(float(ai[:, 0].mean()), 6),
+                "detection_auc_min": round(float(ai[:, 1].min()), 6),
+                "note": ("N concurrent one-GPU 10-client federations (run r on rank r, as the reference's "
+                         "runs loop src/main.py:108-110); aggregate = N x steps / slowest rank's time")}
     if rec is not None:
         line = json.dumps(rec)
         os.write(real_stdout, (line + "\n").encode())

@@ -457,7 +457,8 @@ class Federation:
         with self.tel.phase("eval"):
             er = eng.evaluate(self.model_type, cfg.metric, keep_latents=cfg.save_latents)
             vec = np.zeros(N, dtype=np.float64)
-            vec[self.local[0]:self.local[-1] + 1] = er.metrics
+            if self.local:   # a rank may host no client (fewer clients than ranks)
+                vec[self.local[0]:self.local[-1] + 1] = er.metrics
         with self.tel.phase("comm"):
             vec = self.comm.all_reduce_sum(vec)
         metrics = np.array(vec, dtype=np.float64)

@@ -11,13 +11,17 @@ repository snapshot to the GPU box.  ``python -m fedmse_decentralized_amd.ops.bu
 rebuilds what is stale.
 
 Staleness is decided by content, not by file times: every library has a
-``<lib>.buildhash`` stamp next to it holding the SHA-256 of its compiler,
-flags and the bytes of every source and header that goes into it.  A library
-whose stamp is missing or differs is rebuilt (a copied tree with fresh mtimes
-rebuilds nothing; an edited source is never hidden by a newer ``.so``).
+``<lib>.buildhash`` stamp next to it holding the SHA-256 of its compiler's
+identity (resolved path + ``--version`` output), flags and the bytes of every
+source and header that goes into it.  A library whose stamp is missing or
+differs is rebuilt (a copied tree with fresh mtimes rebuilds nothing; an
+edited source is never hidden by a newer ``.so``; a different toolchain on
+the machine that imports the tree rebuilds).  ``BUILD_STATUS`` records, per
+library, whether this process compiled it or reused it and under which hash.
 """
 from __future__ import annotations
 
+import functools
 import hashlib
 import os
 import shutil
@@ -32,6 +36,24 @@ HOST_LIB = LIBDIR / "libfedmx_host.so"
 HIP_LIB = LIBDIR / "libfedmx_hip.so"
 HIP_STAMPS_LIB = LIBDIR / "libfedmx_hip_stamps.so"
 OFFLOAD_ARCH = os.environ.get("FEDMX_OFFLOAD_ARCH", "gfx950")
+
+# target path -> (action "compiled" | "reused", content hash) for this process
+BUILD_STATUS: dict = {}
+
+
+@functools.lru_cache(maxsize=None)
+def compiler_identity(exe: str) -> str:
+    """Resolved path and ``--version`` banner of a compiler: part of every
+    build hash, so a library built by another toolchain counts as stale."""
+    path = shutil.which(exe) or exe
+    real = os.path.realpath(path)
+    try:
+        r = subprocess.run([real, "--version"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                           timeout=60)
+        ver = r.stdout.strip()
+    except (OSError, subprocess.SubprocessError) as e:
+        ver = f"unavailable: {e}"
+    return f"{real}\n{ver}"
 
 
 def _sources(sub: str, exts):
@@ -76,22 +98,39 @@ def _run(cmd, cwd=None):
     return r.stdout
 
 
+def _build(target: Path, digest: str, cmd_for, force: bool, verbose: bool) -> Path:
+    """Compile ``target`` unless its stamp already matches ``digest``.  The
+    check-and-compile runs under an exclusive lock on ``<lib>.lock``, so ranks
+    or tests that import a stale tree at once compile it once; the others
+    find it fresh and reuse it.  ``cmd_for(tmp)`` gives the compile command
+    writing to a per-process temporary file, renamed into place atomically."""
+    if not force and not _stale(target, digest):
+        BUILD_STATUS[target] = ("reused", digest)
+        return target
+    import fcntl
+
+    target.parent.mkdir(parents=True, exist_ok=True)
+    with open(target.with_name(target.name + ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and not _stale(target, digest):   # another process built it meanwhile
+            BUILD_STATUS[target] = ("reused", digest)
+            return target
+        tmp = target.with_name(f"{target.name}.{os.getpid()}.tmp")
+        out = _run(cmd_for(tmp))
+        os.replace(tmp, target)
+        _stamp(target, digest)
+    BUILD_STATUS[target] = ("compiled", digest)
+    if verbose:
+        print(out, end="")
+    return target
+
+
 def build_host(force: bool = False, verbose: bool = False) -> Path:
     srcs = _sources("host", (".cpp",))
     cxx = os.environ.get("CXX", "g++")
     flags = [cxx, "-std=c++17", "-O3", "-fPIC", "-shared", "-pthread", "-Wall"]
-    digest = content_hash(flags + [p.name for p in srcs], srcs + _headers())
-    if not force and not _stale(HOST_LIB, digest):
-        return HOST_LIB
-    LIBDIR.mkdir(parents=True, exist_ok=True)
-    tmp = HOST_LIB.with_suffix(".so.tmp")
-    cmd = flags + [*map(str, srcs), "-o", str(tmp)]
-    out = _run(cmd)
-    os.replace(tmp, HOST_LIB)
-    _stamp(HOST_LIB, digest)
-    if verbose:
-        print(out, end="")
-    return HOST_LIB
+    digest = content_hash([compiler_identity(cxx)] + flags + [p.name for p in srcs], srcs + _headers())
+    return _build(HOST_LIB, digest, lambda tmp: flags + [*map(str, srcs), "-o", str(tmp)], force, verbose)
 
 
 def hipcc_path() -> str:
@@ -113,25 +152,24 @@ def build_hip(force: bool = False, verbose: bool = False, extra_flags=(), target
     # optimizer tail: -3.3% launch time measured)
     flags = [f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
              "-ffp-contract=off", "-munsafe-fp-atomics", "-mllvm", "-amdgpu-mfma-vgpr-form=1", *extra_flags]
-    digest = content_hash(["hipcc", *flags, *(p.name for p in srcs)], srcs + _headers())
-    if not force and not _stale(target, digest):
-        return target
-    LIBDIR.mkdir(parents=True, exist_ok=True)
-    tmp = target.with_suffix(".so.tmp")
-    cmd = [hipcc_path(), *flags, f"-I{CSRC / 'hip'}", *map(str, srcs), "-o", str(tmp)]
-    out = _run(cmd)
-    os.replace(tmp, target)
-    _stamp(target, digest)
-    if verbose:
-        print(out, end="")
-    return target
+    digest = content_hash([compiler_identity(hipcc_path()), *flags, *(p.name for p in srcs)], srcs + _headers())
+    return _build(target, digest,
+                  lambda tmp: [hipcc_path(), *flags, f"-I{CSRC / 'hip'}", *map(str, srcs), "-o", str(tmp)],
+                  force, verbose)
 
 
 def build_all(force: bool = False, verbose: bool = False):
     return build_host(force, verbose), build_hip(force, verbose)
 
 
+def describe(target: Path) -> str:
+    """``compiled <lib> (hash …)`` or ``reused <lib> (hash …)`` for a library
+    this process built or checked."""
+    act, digest = BUILD_STATUS.get(target, ("not built", ""))
+    return f"{act} {target} (hash {digest[:16]})" if digest else f"{act} {target}"
+
+
 if __name__ == "__main__":
     force = "--force" in sys.argv
     for p in build_all(force=force, verbose=True):
-        print("built", p)
+        print(describe(p))

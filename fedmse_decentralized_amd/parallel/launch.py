@@ -2,8 +2,9 @@
 
 Reads RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT from the
 environment.  On ROCm the ``nccl`` backend is RCCL; for multi-process CPU
-tests use ``gloo``.  ``HSA_ENABLE_IPC_MODE_LEGACY=0`` must stay exported for
-RCCL's dmabuf IPC on this platform.
+tests use ``gloo``.  ``HSA_ENABLE_IPC_MODE_LEGACY=0`` must be exported for
+RCCL's dmabuf IPC on this platform, before the HIP runtime starts
+(``parallel/env.py``; the entry points export it before importing torch).
 """
 from __future__ import annotations
 
@@ -14,6 +15,7 @@ from typing import Optional
 import torch
 
 from .comm import Comm, LoopbackComm, TorchDistComm
+from .env import export_comm_env
 
 
 def env_world() -> int:
@@ -47,11 +49,14 @@ def init_comm(backend: Optional[str] = None, device: Optional[str] = None, timeo
 
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    # the exchange buffers are persistent; without this, ProcessGroupNCCL's
-    # recordStream on every collective's tensors leaves events that the caching
-    # allocator then polls on each later allocation of the round loop
-    os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
+    # normally already exported by the entry point before HIP started
+    # (parallel/env.py); set late, HSA never sees it
+    late = export_comm_env()
+    if late and device == "cuda" and torch.cuda.is_initialized():
+        import sys
+
+        print(f"warning: {', '.join(late)} set after the HIP runtime started; export it before launching "
+              "(bench.py / main.py do this before importing torch)", file=sys.stderr)
     if backend is None:
         # FEDMX_DIST_BACKEND=gloo: multi-rank rehearsal on one GPU (RCCL needs distinct GPUs)
         backend = os.environ.get("FEDMX_DIST_BACKEND") or ("nccl" if device == "cuda" else "gloo")

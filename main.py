@@ -18,21 +18,27 @@ import argparse
 import logging
 import sys
 
-from fedmse_decentralized_amd.io.files import reserve_fd_table
+from fedmse_decentralized_amd.parallel.env import export_comm_env
+
+# RCCL's transport settings reach HSA only if exported before the HIP runtime
+# starts (parallel/env.py); nothing has touched the GPU yet
+export_comm_env()
+
+from fedmse_decentralized_amd.io.files import reserve_fd_table  # noqa: E402
 
 # grow the descriptor table while the process is still single-threaded
 # (io.files.reserve_fd_table: later growth waits on RCU in threaded processes)
 reserve_fd_table()
 
-import torch
+import torch  # noqa: E402
 
-from fedmse_decentralized_amd.config import ExperimentConfig, add_arguments, from_args
-from fedmse_decentralized_amd.federation import Federation
-from fedmse_decentralized_amd.io import reports
-from fedmse_decentralized_amd.parallel.comm import LoopbackComm
-from fedmse_decentralized_amd.parallel.launch import init_comm, shutdown
-from fedmse_decentralized_amd.protocol.early_stop import GlobalEarlyStop
-from fedmse_decentralized_amd.utils.logging import setup_logging
+from fedmse_decentralized_amd.config import ExperimentConfig, add_arguments, from_args  # noqa: E402
+from fedmse_decentralized_amd.federation import Federation  # noqa: E402
+from fedmse_decentralized_amd.io import reports  # noqa: E402
+from fedmse_decentralized_amd.parallel.comm import LoopbackComm  # noqa: E402
+from fedmse_decentralized_amd.parallel.launch import init_comm, shutdown  # noqa: E402
+from fedmse_decentralized_amd.protocol.early_stop import GlobalEarlyStop  # noqa: E402
+from fedmse_decentralized_amd.utils.logging import setup_logging  # noqa: E402
 
 
 def run_sweep(cfg: ExperimentConfig, comm=None) -> dict:
@@ -68,6 +74,12 @@ def run_sweep(cfg: ExperimentConfig, comm=None) -> dict:
     parallel = cfg.parallel_combos and comm.world_size > 1
     results = []
     if cfg.concurrent_combos and not parallel:
+        if comm.world_size > 1:
+            # each concurrent federation issues its collectives from its own
+            # HIP stream; the exchange channels (RCCL communicator, IPC
+            # seq/parity slots) assume one ordered stream per rank
+            raise SystemExit("--concurrent-combos runs every combination in ONE process on one GPU; with "
+                             f"{comm.world_size} ranks use --parallel-combos (one combination per rank) instead")
         if cfg.compat != "fixed":
             raise SystemExit("--concurrent-combos needs --compat fixed (the reference's early-stop state is "
                              "shared across combinations run in sequence)")

@@ -166,6 +166,48 @@ def test_device_round_multi_rank_one_gpu(tmp_path, world):
         assert d["params"] == ref_params[loc[0]:loc[-1] + 1]
 
 
+def _edge_worker(rank, world, port, out, n_clients):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), FEDMX_DEVICE_INDEX="0", HSA_ENABLE_IPC_MODE_LEGACY="0",
+                      FEDMX_COMM_SELFTEST="0")
+    _shrink()
+    from fedmse_decentralized_amd.parallel.launch import init_comm, shutdown
+
+    comm = init_comm(backend="gloo", device="cuda")
+    fed, res = _run(_cfg(os.path.join(out, f"r{rank}"), network_size=n_clients, save_checkpoints=False,
+                         debug_replica_check=True), "mse_avg", 3, comm=comm)
+    res["fast"] = fed._fast is not None
+    res["params"] = fed.engine.store.params.double().sum(1).tolist()
+    res["local"] = fed.local
+    with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
+        json.dump(res, f)
+    shutdown(comm)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n_clients", [10, 8, 4],
+                         ids=["10-clients-over-8-ranks", "one-client-per-rank", "ranks-without-clients"])
+def test_device_round_eight_ranks_edge_shapes(tmp_path, n_clients):
+    """The device protocol in the shapes the first 8-GPU run meets (VERDICT r3
+    Next #5): 8 gloo ranks sharing GPU 0 run the headline 10-client federation
+    (most ranks have no selected client in a round), one client per rank
+    (BASELINE config 3) and 4 clients (ranks hosting none).  Every rank must
+    match the single-process device round's decisions and AUCs."""
+    out = str(tmp_path)
+    mp.start_processes(_edge_worker, args=(8, _port(), out, n_clients), nprocs=8, join=True, start_method="spawn")
+    _shrink()
+    fed, ref = _run(_cfg(os.path.join(out, "single"), network_size=n_clients, save_checkpoints=False), "mse_avg", 3)
+    ref_params = fed.engine.store.params.double().sum(1).tolist()
+    for r in range(8):
+        d = json.load(open(os.path.join(out, f"rank{r}.json")))
+        assert d["fast"]
+        assert d["agg"] == ref["agg"] and d["sel"] == ref["sel"] and d["ver"] == ref["ver"]
+        for x, y in zip(d["metrics"], ref["metrics"]):
+            np.testing.assert_array_equal(np.array(x), np.array(y))
+        loc = d["local"]
+        assert d["params"] == (ref_params[loc[0]:loc[-1] + 1] if loc else [])
+
+
 def test_device_round_is_deterministic(tmp_path):
     """Run-to-run determinism: two identical device-protocol
     runs give bit-identical parameters, Adam state and metrics."""

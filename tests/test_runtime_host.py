@@ -44,3 +44,33 @@ def test_build_staleness_is_content_based(tmp_path):
     for target in (build.HOST_LIB, build.HIP_LIB):
         if target.exists() and build._hash_path(target).exists():
             assert len(build._hash_path(target).read_text().strip()) == 64
+
+
+def test_compiler_identity_is_part_of_the_build_hash(tmp_path, monkeypatch):
+    """VERDICT r3 Next #6: a library built by another toolchain is stale.  The
+    recorded compiler identity (resolved path + --version) enters the hash,
+    so changing it marks the in-tree library stale; build_hip then reports
+    'compiled' rather than 'reused'."""
+    from fedmse_decentralized_amd.ops import build
+
+    ident = build.compiler_identity(build.hipcc_path())
+    assert "/" in ident.splitlines()[0] and len(ident.splitlines()) > 1   # path + version banner
+    srcs = build._sources("hip", (".hip",)) + build._headers()
+    d_real = build.content_hash([ident, "-O3"], srcs)
+    d_other = build.content_hash([ident.replace("\n", "\nother toolchain ", 1), "-O3"], srcs)
+    assert d_real != d_other
+    # a real build whose stamp came from another compiler identity is rebuilt
+    lib = tmp_path / "libfake.so"
+    calls = []
+    monkeypatch.setattr(build, "LIBDIR", tmp_path)
+    monkeypatch.setattr(build, "_run", lambda cmd, cwd=None: (calls.append(cmd), open(cmd[-1], "wb").close())[1]
+                        or "")
+    build.build_hip(target=lib)
+    assert build.BUILD_STATUS[lib][0] == "compiled" and len(calls) == 1
+    build.build_hip(target=lib)
+    assert build.BUILD_STATUS[lib][0] == "reused" and len(calls) == 1
+    assert build.describe(lib).startswith("reused ")
+    build.compiler_identity.cache_clear()
+    monkeypatch.setattr(build, "compiler_identity", lambda exe: "/opt/other/hipcc\nother clang 99")
+    build.build_hip(target=lib)
+    assert build.BUILD_STATUS[lib][0] == "compiled" and len(calls) == 2
