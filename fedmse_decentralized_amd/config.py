@@ -50,6 +50,13 @@ class ExperimentConfig:
     fedprox_mu: float = 0.001
     verification_threshold: float = 3.0
     performance_threshold: float = 0.002
+    # > 0 (fixed-mode option, not the reference): the verifier's drift limit is
+    #   RELATIVE, drift <= drift_threshold_rel x sum_tensors ||history||_2,
+    #   instead of the absolute verification_threshold.  The absolute 3.0
+    #   (model_verifier.py:72-75) was tuned for the reference's 10 clients;
+    #   a large federation's early aggregates move further and were rejected
+    #   by nearly every receiver (profiles/r4_adoption_ablation.md).
+    drift_threshold_rel: float = 0.0
     max_aggregation: int = 3
     max_rejected_updates: int = 3
     vote_batch_size: int = 128
@@ -81,7 +88,9 @@ class ExperimentConfig:
     election: str = "first_voter"
     # "decentralized": receivers verify the broadcast aggregate (reference);
     # "centralized": server push, every client adopts the aggregate (legacy
-    #   GlobalAggregator.update).
+    #   GlobalAggregator.update);
+    # "local": ablation, no aggregation at all (selected clients train, every
+    #   client is evaluated; profiles/r4_adoption_ablation.md).
     aggregation_mode: str = "decentralized"
     # "code": ModelVerifier rule (drift <= 3.0 and dperf >= -0.002);
     # "thesis": the thesis variant (Thesis p.20-26): loss-ratio acceptance

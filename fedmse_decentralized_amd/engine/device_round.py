@@ -234,6 +234,7 @@ class DeviceRound:
         self.thesis = cfg.protocol_variant == "thesis"
         self.elect_mode = (1 if cfg.election == "majority" else 0) | (6 if self.thesis else 0)
         self.centralized = cfg.aggregation_mode == "centralized"
+        self.drift_rel = cfg.drift_threshold_rel > 0   # kernel mode 3: drift <= rel x ||history||
         self.pending: deque = deque()
         # optional: HIP-event time of every round's training launch (bench.py
         # at N > 1 measures the wait for the slowest rank's largest client)
@@ -509,10 +510,12 @@ class DeviceRound:
                                 seg=eng._seg.data_ptr(), agg_counts=self.agg_counts.data_ptr(),
                                 has_hist=self.has_hist.data_ptr(), hist_perf=self.hist_perf.data_ptr(),
                                 rejected=self.rejected.data_ptr(), rej_out=side_rep.data_ptr() + 8 * N,
-                                thr=float(cfg.thesis_loss_ratio if self.thesis else cfg.verification_threshold),
+                                thr=float(cfg.thesis_loss_ratio if self.thesis else
+                                          (cfg.drift_threshold_rel if self.drift_rel else cfg.verification_threshold)),
                                 pthr=float(cfg.performance_threshold),
                                 start=self.start, n_local=self.n_local, P=P_PAD, d_in=fed.dims.d_in,
-                                mode=1 if self.centralized else (2 if self.thesis else 0), pad=0)
+                                mode=1 if self.centralized else (2 if self.thesis else (3 if self.drift_rel else 0)),
+                                pad=0)
             if self.fused_verify:
                 # verification forward, decisions, adoption and the evaluation /
                 # artefact snapshots in one launch (bit-identical to the

@@ -183,7 +183,7 @@ class Federation:
             self.verifier = ThesisVerifier(cfg.thesis_loss_ratio, cfg.verification_method, cfg.max_rejected_updates)
         else:
             self.verifier = Verifier(cfg.verification_threshold, cfg.performance_threshold,
-                                     cfg.verification_method, cfg.max_rejected_updates)
+                                     cfg.verification_method, cfg.max_rejected_updates, cfg.drift_threshold_rel)
         # thesis variant: random aggregator fallback (own stream: the reference RNG order is untouched)
         self.fallback_rng = random.Random(cfg.data_seed + 7919 * (self.run + 1)) \
             if cfg.protocol_variant == "thesis" else None
@@ -339,6 +339,9 @@ class Federation:
                 selected = [c for c in selected if c not in cfg.dropped_clients]
         if self._fast is not None:
             return self._fast.enqueue(selected)
+        # aggregation_mode "local": local-training-only ablation (same
+        # selections, training and evaluation; no election, no aggregate)
+        local_only = cfg.aggregation_mode == "local"
         with self.tel.phase("select"):
             local_sel = [c for c in selected if self._mine(c)]
             local_rows = [self._loc(c) for c in local_sel]
@@ -399,9 +402,12 @@ class Federation:
                 k = len(selected)
                 noise = _TableNoise([float(u) for u in self.noise.rand_n(k * (k - 1))])
             fb = OneDraw(self.fallback_rng.random()) if self.fallback_rng is not None else None
-            el = elect(selected, base_scores, self.agg_counts, cfg.max_aggregation, noise,
-                       log_enabled=info, vote_mse_cap=cap, fallback_rng=fb)
-            aggregator = el.aggregator
+            if local_only:
+                aggregator = None   # ablation: nobody aggregates, nobody adopts
+            else:
+                el = elect(selected, base_scores, self.agg_counts, cfg.max_aggregation, noise,
+                           log_enabled=info, vote_mse_cap=cap, fallback_rng=fb)
+                aggregator = el.aggregator
 
         verification_results: List[Dict] = []
         if aggregator is not None:
@@ -449,7 +455,7 @@ class Federation:
                                  f"(Rejected updates: {r_['rejected_updates']})")
                 vr = verification_results
                 self.writer.submit(lambda vr=vr, rnd=rnd: self._report_verification(rnd, vr))
-        else:
+        elif not local_only:
             log.warning("No aggregator selected for this round")
 
         # ---------------- evaluation of every hosted client (batched launches)
@@ -515,6 +521,11 @@ class Federation:
             own = eng.model_mse([self._loc(c) for c in receivers], [data_of[key_of[c]] for c in receivers])
             old_loss = {c: float(x) for c, x in zip(receivers, own)}
         drift = {v: float(x) for v, x in zip(need, drift_np)}
+        hnorm = {}
+        if need and cfg.drift_threshold_rel > 0 and not thesis:
+            # relative drift limit: sum_tensors ||history||_2 of each history version
+            hn = eng.fetch([eng.param_drift(hist, torch.zeros_like(agg))])[0]
+            hnorm = {v: float(x) for v, x in zip(need, hn)}
         accept = []
         vec = np.zeros((N, 2), dtype=np.float64)
         for c in receivers:
@@ -523,7 +534,8 @@ class Federation:
                 dec = self.verifier.decide_losses(c, vs_, version, old_loss[c], new_loss[key_of[c]], rnd)
             else:
                 dr = drift.get(vs_.history_version, 0.0) if vs_.history_version is not None else 0.0
-                dec = self.verifier.decide(c, vs_, version, perf[key_of[c]], dr, rnd)
+                dec = self.verifier.decide(c, vs_, version, perf[key_of[c]], dr, rnd,
+                                           hist_norm=hnorm.get(vs_.history_version))
             self.verifier.apply(c, vs_, dec)
             if dec.verified:
                 accept.append(c)

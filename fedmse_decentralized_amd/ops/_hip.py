@@ -41,6 +41,7 @@ TRAIN_FLAG_NO_HELPER = 4
 _HELPER_ENV = os.environ.get("FEDMX_TRAIN_HELPER")
 TRAIN_HELPER = None if _HELPER_ENV is None else _HELPER_ENV != "0"
 _lib = None
+_lib_path: Optional[Path] = None
 
 FWD_DTYPE = np.dtype([
     ("params", "<u8"), ("x", "<u8"), ("sse", "<u8"), ("lat", "<u8"),
@@ -125,6 +126,8 @@ def lib():
             if not path.exists() and not override:
                 build.build_hip()   # hipcc cross-compiles for gfx950 in-tree
             L = ctypes.CDLL(str(path))
+            global _lib_path
+            _lib_path = path
             vp, i32 = ctypes.c_void_p, ctypes.c_int
             sig = {
                 "fedmx_forward_rows": [vp, i32, vp],
@@ -171,6 +174,12 @@ def lib():
             assert L.fedmx_ipc_max_world() == IPC_MAX_WORLD and L.fedmx_ipc_max_chunks() == IPC_MAX_CHUNKS
             _lib = L
     return _lib
+
+
+def lib_path() -> str:
+    """Path of the kernel library this process loaded (FEDMX_HIP_LIB variants)."""
+    lib()
+    return str(_lib_path)
 
 
 def _check(rc: int, what: str):

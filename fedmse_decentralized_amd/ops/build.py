@@ -35,6 +35,8 @@ LIBDIR = HERE / "lib"
 HOST_LIB = LIBDIR / "libfedmx_host.so"
 HIP_LIB = LIBDIR / "libfedmx_hip.so"
 HIP_STAMPS_LIB = LIBDIR / "libfedmx_hip_stamps.so"
+# IEEE-division Adam variant (-DFEDMX_EXACT_ADAM=1): long-horizon parity test
+HIP_EXACT_LIB = LIBDIR / "libfedmx_hip_exact.so"
 OFFLOAD_ARCH = os.environ.get("FEDMX_OFFLOAD_ARCH", "gfx950")
 
 # target path -> (action "compiled" | "reused", content hash) for this process
@@ -159,7 +161,11 @@ def build_hip(force: bool = False, verbose: bool = False, extra_flags=(), target
 
 
 def build_all(force: bool = False, verbose: bool = False):
-    return build_host(force, verbose), build_hip(force, verbose)
+    """The host runtime, the kernel library, and its IEEE-Adam variant (loaded
+    only by tests/test_long_horizon_gpu.py through FEDMX_HIP_LIB)."""
+    out = build_host(force, verbose), build_hip(force, verbose)
+    build_hip(force, verbose, extra_flags=["-DFEDMX_EXACT_ADAM=1"], target=HIP_EXACT_LIB)
+    return out
 
 
 def describe(target: Path) -> str:

@@ -333,7 +333,9 @@ struct DecideArgs {
                            //    included, loads the aggregate and re-anchors FedProx, no verification;
                            // 2: thesis rule (Thesis p.20-22 Alg. 4.3): accept iff the aggregate's
                            //    MSE on the receiver's data is finite and <= (1 + thr) x the MSE of
-                           //    the receiver's own current model there (fused kernel only)
+                           //    the receiver's own current model there (fused kernel only);
+                           // 3: as 0 with a RELATIVE drift threshold: accept iff
+                           //    drift <= thr x sum_tensors ||history||_2 and dperf >= -pthr
   int32_t pad;
 };
 static_assert(sizeof(DecideArgs) == 152, "DecideArgs layout is shared with Python");
@@ -386,33 +388,48 @@ __global__ __launch_bounds__(1024) void decide_adopt_kernel(const DecideArgs A) 
     mse = n > 0 ? tot / ((double)n * A.d_in) : __builtin_nan("");
   }
   // ---- drift of the receiver's history vs the aggregate (param_drift)
-  float drift = 0.f;
+  float drift = 0.f, hnorm = 0.f;
+  const bool rel = A.mode == 3;
+  __shared__ float part_h[8][16];
   if (had_hist) {
     const float* h = A.hist + off;
-    float acc[8];
+    float acc[8], acch[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc[t] = 0.f;
+    for (int t = 0; t < 8; ++t) acc[t] = acch[t] = 0.f;
     for (int p = tid; p < A.P; p += blockDim.x) {
       const int sg = A.seg[p];
       const float df = h[p] - A.agg[p];
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] += (sg == t) ? df * df : 0.0f;
+      if (rel) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acch[t] += (sg == t) ? h[p] * h[p] : 0.0f;
+      }
     }
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const float v = wave_sum(acc[t]);
       if (lane == 0) part[t][wv] = v;
+      if (rel) {
+        const float vh = wave_sum(acch[t]);
+        if (lane == 0) part_h[t][wv] = vh;
+      }
     }
     __syncthreads();
     if (tid == 0) {
       const int nw = blockDim.x >> 6;
-      float tot = 0.f;
+      float tot = 0.f, toth = 0.f;
       for (int t = 0; t < 8; ++t) {
-        float s2 = 0.f;
-        for (int w = 0; w < nw; ++w) s2 += part[t][w];
+        float s2 = 0.f, h2 = 0.f;
+        for (int w = 0; w < nw; ++w) {
+          s2 += part[t][w];
+          if (rel) h2 += part_h[t][w];
+        }
         tot += sqrtf(s2);
+        toth += sqrtf(h2);
       }
       drift = tot;
+      hnorm = toth;
     }
   }
   if (tid == 0) {
@@ -423,7 +440,8 @@ __global__ __launch_bounds__(1024) void decide_adopt_kernel(const DecideArgs A) 
       A.has_hist[cl] = 1;
     } else {
       const double change = perf - A.hist_perf[cl];
-      ok = ((double)drift <= A.thr) && (change >= -A.pthr);
+      const double lim = rel ? A.thr * (double)hnorm : A.thr;
+      ok = ((double)drift <= lim) && (change >= -A.pthr);
     }
     A.hist_perf[cl] = perf;
     const int rj = ok ? 0 : A.rejected[cl] + 1;
@@ -481,6 +499,7 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
   __shared__ int s_ok;
   __shared__ double s_d[4];
   __shared__ float part[8][16];
+  __shared__ float part_h[8][16];
   const int a = A.state[0];
   if (a >= 0 && blockIdx.x == 0 && threadIdx.x == 0) A.agg_counts[a] += 1;
   if ((int)blockIdx.x >= A.n_local) {
@@ -558,12 +577,13 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     // summing p = vt, vt + 1024, ... in increasing order).  All of a
     // thread's loads are issued before the first add: one memory round trip
     // instead of one per 4 elements (6 dependent rounds, ~5 us of the kernel).
-    float drift = 0.f;
-    if (had_hist && A.mode == 0 && !(FEDMX_VERIFY_ABLATE & 2)) {
+    float drift = 0.f, hnorm = 0.f;
+    const bool rel = A.mode == 3;
+    if (had_hist && (A.mode == 0 || rel) && !(FEDMX_VERIFY_ABLATE & 2)) {
       const float* h = A.hist + off;
       constexpr int NJ = (P_PAD + 1023) / 1024;
       int sg[2][NJ];
-      float df[2][NJ];
+      float df[2][NJ], hv[2][NJ];
 #pragma unroll
       for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -571,9 +591,11 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
           const int p = tid + 512 * q + 1024 * j;
           sg[q][j] = -1;
           df[q][j] = 0.f;
+          hv[q][j] = 0.f;
           if (p < P_PAD) {
             sg[q][j] = A.seg[p];
-            df[q][j] = h[p] - A.agg[p];
+            hv[q][j] = h[p];
+            df[q][j] = hv[q][j] - A.agg[p];
           }
         }
 #pragma unroll
@@ -590,16 +612,34 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
           const float v = wave_sum(acc[t]);
           if (lane == 0) part[t][wv + 8 * q] = v;
         }
+        if (rel) {   // relative threshold: the history's own per-tensor norms, same order
+#pragma unroll
+          for (int t = 0; t < 8; ++t) acc[t] = 0.f;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc[t] += (sg[q][j] == t) ? hv[q][j] * hv[q][j] : 0.0f;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const float v = wave_sum(acc[t]);
+            if (lane == 0) part_h[t][wv + 8 * q] = v;
+          }
+        }
       }
       __syncthreads();
       if (tid == 0) {
-        float tot = 0.f;
+        float tot = 0.f, toth = 0.f;
         for (int t = 0; t < 8; ++t) {
-          float s2 = 0.f;
-          for (int w = 0; w < 16; ++w) s2 += part[t][w];
+          float s2 = 0.f, h2 = 0.f;
+          for (int w = 0; w < 16; ++w) {
+            s2 += part[t][w];
+            if (rel) h2 += part_h[t][w];
+          }
           tot += sqrtf(s2);
+          toth += sqrtf(h2);
         }
         drift = tot;
+        hnorm = toth;
       }
     }
     if (tid == 0) {
@@ -613,7 +653,8 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
         A.has_hist[cl] = 1;
       } else {
         const double change = perf - A.hist_perf[cl];
-        okk = ((double)drift <= A.thr) && (change >= -A.pthr);
+        const double lim = rel ? A.thr * (double)hnorm : A.thr;
+        okk = ((double)drift <= lim) && (change >= -A.pthr);
       }
       A.hist_perf[cl] = perf;
       const int rj = okk ? 0 : A.rejected[cl] + 1;

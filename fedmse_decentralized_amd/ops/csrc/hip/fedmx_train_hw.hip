@@ -46,6 +46,17 @@
 #ifndef FEDMX_HW_PACKED
 #define FEDMX_HW_PACKED 0
 #endif
+// 1: barrier #1 is a main-waves-only LDS flag exchange and each helper hands
+// W4(s+1) / its Adam scalars to its main wave through an LDS flag the main
+// waits on right before layer 4, instead of through barrier #1.  The
+// helpers then no longer gate the mains' layer-1 exchange: their W4 gradient
+// + Adam window runs from barrier #2 of step s to layer 4 of step s+1.
+#ifndef FEDMX_HW_FLAGS
+#define FEDMX_HW_FLAGS 0
+#endif
+// bound on one flag wait (polls); a wait that runs out marks the launch failed
+// (epochs_run = -1000) instead of hanging the GPU
+constexpr int HW_SPIN_LIMIT = 1 << 22;
 // (Round 3 also measured, and removed, seven schedule variants of this step --
 // dH3 partial reads in flight together, the bias column by address select,
 // helper-formed next-step Adam scalars, a software-pipelined tail, helper
@@ -181,8 +192,28 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   float* const sQ4 = sRedDH3 + L_RED + 4 * L_SCR;   // [w][v][t][lane][4]
   double* const sLoss = reinterpret_cast<double*>(sQ4 + L_Q4);  // [8 waves][4]
   // per-step Adam scalars (helper -> main), double-buffered by step parity:
-  // [neg_step_size, inv_bc2s, bc2s, -]
+  // [neg_step_size, inv_bc2s, bc2s, -]; FEDMX_HW_FLAGS: one pair per helper
   float* const sK = reinterpret_cast<float*>(sLoss + 32);
+  // FEDMX_HW_FLAGS: [0..3] layer-1 partials of step count v written by main w;
+  // [4..7] W4 / Adam scalars for step count v published by helper w
+  int* const sFlag = reinterpret_cast<int*>(sK + 32);
+  bool spin_fail = false;
+  auto flag_set = [&](int i, int v) {
+    if (lane == 0) __hip_atomic_store(sFlag + i, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  auto flag_wait = [&](int i0, int n, int v) {
+    for (int it = 0;; ++it) {
+      int m = __hip_atomic_load(sFlag + i0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int j = 1; j < n; ++j)
+        m = min(m, __hip_atomic_load(sFlag + i0 + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (m >= v) break;
+      if (it >= HW_SPIN_LIMIT) {
+        spin_fail = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
 
   Lane L;
   L.w1 = sW1 + c * S_W1 + 32 * w + 4 * g;
@@ -486,6 +517,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // (m, v, [anchor], params) in one memory round trip, then each tensor
   // passes through the masters in turn (the barrier sequence of one global_to_masters_o pass per tensor)
   HSTAMP(true, 28);
+  if (FEDMX_HW_FLAGS && threadIdx.x < 8) sFlag[threadIdx.x] = 0;   // (the staging barriers follow)
   f32x4 pv_m[STAGE_PER_THREAD], pv_v[STAGE_PER_THREAD], pv_a[STAGE_PER_THREAD], pv_p[STAGE_PER_THREAD];
   if (stager) {
     stage_load(Mg, pv_m);
@@ -528,23 +560,28 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     int js = 0;   // step index within the launch
     auto publish_k = [&]() {
       next_constants();
-      if (lane == 0 && w8 == 4)
+      if (FEDMX_HW_FLAGS) {
+        if (lane == 0) lds_write4(sK + 8 * w + 4 * (js & 1), f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f});
+      } else if (lane == 0 && w8 == 4) {
         lds_write4(sK + 4 * (js & 1), f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f});
+      }
     };
     publish_k();   // step 0's
+    if (FEDMX_HW_FLAGS) flag_set(4 + w, 1);   // W4 / scalars of launch step 0 published
     for (int ep = 0; ep < A.epochs; ++ep) {
       double acc_tr = 0.0;
       // W4 gradient + Adam between barrier #2 of step s and barrier #1 of s+1
       for (int bi = 0; bi < nb; ++bi) {
         const bool hs = (ep == 0 && bi == STAMP_STEP);
         HSTAMP(hs, 0);
-        __syncthreads();   // barrier #1 (main: layer-1 partials)
+        if (!FEDMX_HW_FLAGS) __syncthreads();   // barrier #1 (main: layer-1 partials)
         HSTAMP(hs, 2);
         __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
         HSTAMP(hs, 7);
         if (FEDMX_HW_ABLATE & 64) {
           ++js;
           publish_k();
+          if (FEDMX_HW_FLAGS) flag_set(4 + w, js + 1);
           continue;
         }
         const f32x4 w4a0 = lds_read4(sT0 + tr);
@@ -586,6 +623,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         publish_q4();
         ++js;
         publish_k();   // step js's scalars, read by the mains after its barrier #1
+        if (FEDMX_HW_FLAGS) flag_set(4 + w, js + 1);   // W4(js) ready for main w's layer 4
         HSTAMP(hs, 11);
       }
       double prox_now = 0.0;
@@ -690,21 +728,26 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         lds_write4(red + (w * 2 + 0) * 256 + lane * 4, l1a);
         lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1b);
         HSTAMP(ms, 1);
-        __syncthreads();  // barrier #1
+        if (FEDMX_HW_FLAGS) {
+          flag_set(w, js + 1);        // (release: the partial writes above complete first)
+          flag_wait(0, 4, js + 1);    // every main wave's partial of this step
+        } else {
+          __syncthreads();  // barrier #1
+        }
         HSTAMP(ms, 2);
-        {
+        auto read_helper_state = [&]() {
           // this step's Adam scalars (helper-published)
-          const f32x4 kk = lds_read4(sK + 4 * (js & 1));
+          const f32x4 kk = lds_read4(FEDMX_HW_FLAGS ? sK + 8 * w + 4 * (js & 1) : sK + 4 * (js & 1));
           K.neg_step_size = kk[0];
           K.inv_bc2s = kk[1];
           K.bc2s = kk[2];
-          ++js;
-        }
-        // W4(s) rows in the dH3 A-operand layout (helper-published)
+          // W4(s) rows in the dH3 A-operand layout (helper-published)
 #pragma unroll
-        for (int v = 0; v < 2; ++v)
+          for (int v = 0; v < 2; ++v)
 #pragma unroll
-          for (int t = 0; t < 2; ++t) q4[v][t] = lds_read4(q4p + (2 * v + t) * 256);
+            for (int t = 0; t < 2; ++t) q4[v][t] = lds_read4(q4p + (2 * v + t) * 256);
+        };
+        if (!FEDMX_HW_FLAGS) read_helper_state();
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           f32x4 s = lds_read4(red + t * 256 + lane * 4);
@@ -748,6 +791,11 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           h3[0] = acc0;
           h3[1] = acc1;
         }
+        if (FEDMX_HW_FLAGS) {
+          flag_wait(4 + w, 1, js + 1);   // helper w has published W4(s) and the scalars
+          read_helper_state();
+        }
+        ++js;
         {
           f32x4 acc0 = zero4(), acc1 = zero4();
           const f32x4 a00 = lds_read4(a4p);
@@ -965,6 +1013,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     A.epochs_run[kslot] = ep_run;
     A.best_epoch[kslot] = best_ep;
   }
+  if (FEDMX_HW_FLAGS && spin_fail && lane == 0) A.epochs_run[kslot] = -1000;   // a flag wait ran out
 }
 
 }  // namespace hw

@@ -8,7 +8,8 @@ and ``ClientTrainer.update_from_peers`` (`src/Trainer/client_trainer.py:174-206`
 * afterwards: ``drift = sum_tensors ||theta_prev_received - theta_new||_2``,
   ``perf = 1 / (1 + MSE(V, model(V)))``, ``dperf = perf_new - perf_prev``;
   accept iff ``drift <= 3.0`` and ``dperf >= -0.002``;  the history is
-  updated to the new model either way;
+  updated to the new model either way (fixed-mode option ``drift_rel``: the
+  limit is ``drift_rel * sum_tensors ||theta_prev_received||_2`` instead);
 * accept: adopt the model, refresh the FedProx anchor, reset the rejection
   counter; reject: increment it, and at ``>= 3`` log a possible attack.
 
@@ -42,8 +43,10 @@ class VerifyDecision:
 
 class Verifier:
     def __init__(self, verification_threshold: float = 3.0, performance_threshold: float = 0.002,
-                 method: str = "val", max_rejected: int = 3):
+                 method: str = "val", max_rejected: int = 3, drift_rel: float = 0.0):
         self.thr = verification_threshold
+        # > 0: relative drift limit drift <= drift_rel * ||history|| (config.drift_threshold_rel)
+        self.drift_rel = drift_rel
         self.perf_thr = performance_threshold
         self.method = method
         self.max_rejected = max_rejected
@@ -52,7 +55,7 @@ class Verifier:
         return st.history_version is not None
 
     def decide(self, client_id: int, st: VerifierState, version: int, perf_new: float, drift: float,
-               current_round: int) -> VerifyDecision:
+               current_round: int, hist_norm: Optional[float] = None) -> VerifyDecision:
         if st.history_version is None:
             st.history_version, st.history_perf, st.history_round = version, perf_new, current_round
             return VerifyDecision(True, 0.0, 0.0)
@@ -61,7 +64,8 @@ class Verifier:
         if log.isEnabledFor(logging.INFO):
             log.info(f"Client {client_id} - Param changes: {drift:.10f}, Performance change: {change:.10f}")
             log.info(f"Using {self.method} dataset for verification")
-        ok = (drift <= self.thr) and (change >= -self.perf_thr)
+        limit = self.drift_rel * hist_norm if self.drift_rel > 0 and hist_norm is not None else self.thr
+        ok = (drift <= limit) and (change >= -self.perf_thr)
         return VerifyDecision(ok, change, drift)
 
     def apply(self, client_id: int, st: VerifierState, dec: VerifyDecision) -> None:

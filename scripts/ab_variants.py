@@ -22,6 +22,10 @@ VARIANTS = {
     # helper delays hd8/16/24, priorities hprio1/3 and (r2) hwprio1/3: all measured slower or
     # neutral (profiles/r3_train_hw_experiments.md); their switches were removed from the kernel
     # (source in git history, commit 5365856)
+    "exact": ["-DFEDMX_EXACT_ADAM=1"],
+    "flags": ["-DFEDMX_HW_FLAGS=1"],                 # r4: mains-only layer-1 exchange + helper->main LDS flags
+    "flags_madam": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=32"],   # timing only: + mains skip W1 Adam
+    "flags_hnone": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=64"],   # timing only: + helpers idle                # r4: IEEE sqrt / division Adam (torch's op sequence)
     "packed": ["-DFEDMX_HW_PACKED=1"],               # packed-fp32 Adam (bit-identical)  966-974 vs 948-951 (+2 %)
     "abl_pf": ["-DFEDMX_HW_ABLATE=8"],               # timing only: prefetch always hits the cache
     "abl_hadam": ["-DFEDMX_HW_ABLATE=16"],           # timing only: helpers skip W4's Adam

@@ -450,6 +450,32 @@ def test_device_round_protocol_variants_match_host_path(tmp_path, election, mode
         assert all(v == [] for v in a["ver"])
 
 
+@pytest.mark.parametrize("rel,fused", [(0.05, True), (0.5, True), (0.05, False)])
+def test_device_round_relative_drift_threshold_matches_host_path(tmp_path, monkeypatch, rel, fused):
+    """drift_threshold_rel (fixed-mode option, profiles/r4_adoption_ablation.md):
+    the device kernels' relative drift limit (mode 3: drift <= rel x
+    sum_tensors ||history||) reaches the host verifier's decisions, on the
+    fused verification kernel and on decide_adopt (fused=False: the fused
+    kernel's row limit forced below the data size)."""
+    from fedmse_decentralized_amd.ops import _hip
+
+    _shrink()
+    if not fused:
+        monkeypatch.setattr(_hip, "VERIFY_MAX_ROWS", 1)
+    kw = dict(save_checkpoints=False, drift_threshold_rel=rel)
+    fa, a = _run(_cfg(str(tmp_path / "dev"), **kw), "mse_avg", 6)
+    fb, b = _run(_cfg(str(tmp_path / "host"), device_protocol=False, **kw), "mse_avg", 6)
+    assert fa._fast is not None and fb._fast is None
+    assert fa._fast.fused_verify == fused
+    assert a["sel"] == b["sel"] and a["agg"] == b["agg"] and a["ver"] == b["ver"]
+    for x, y in zip(a["metrics"], b["metrics"]):
+        np.testing.assert_array_equal(np.array(x), np.array(y))
+    assert torch.equal(fa.engine.store.params, fb.engine.store.params)
+    rejected = sum(1 for v in a["ver"] for d in v if not d["is_verified"])
+    if rel == 0.05:
+        assert rejected > 0   # a tight limit does reject
+
+
 @pytest.mark.parametrize("model_type", ["hybrid", "autoencoder"])
 def test_device_round_classification_metric_matches_host_path(tmp_path, model_type):
     """--metric classification (F1 at threshold 0.5, the reference
