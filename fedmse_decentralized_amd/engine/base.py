@@ -101,7 +101,10 @@ class ClientStore:
 
     # zero rows after the last client's training rows: the helper-wave
     # kernel's batch loads (batch <= 12) read whole 12-row chunks without
-    # clamping rows past a client's end (those columns are masked)
+    # clamping rows past a client's end (those columns are masked).  Contract
+    # checked by ops/_hip.TrainBuffers before the first launch on a store:
+    # >= 11 rows after the last client, column DP-1 of train/valid holding 1
+    # (``bias_column_rows`` records which buffers _concat filled).
     TRAIN_TAIL_ROWS = 16
 
     @staticmethod
@@ -124,6 +127,7 @@ class ClientStore:
         self.train, self.train_off = self._concat(train, self.device, bias_column=True,
                                                   tail_rows=self.TRAIN_TAIL_ROWS)
         self.valid, self.valid_off = self._concat(valid, self.device, bias_column=True)
+        self.bias_column_rows = ("train", "valid")
         self.test, self.test_off = self._concat(test, self.device)
         lab = np.concatenate([np.asarray(l, dtype=np.int32) for l in test_label]) if test_label else np.zeros(0, np.int32)
         self.test_label = torch.from_numpy(lab).to(self.device)

@@ -113,7 +113,9 @@ class MappedBuffer:
     def __init__(self, nbytes: int):
         L = rt()
         hp = ctypes.c_void_p()
-        rc = L.hipHostMalloc(ctypes.byref(hp), nbytes, hipHostMallocMapped | hipHostMallocCoherent)
+        # (at least 64 bytes: a rank hosting no client asks for empty rings,
+        # and a zero-byte mapping has no device pointer)
+        rc = L.hipHostMalloc(ctypes.byref(hp), max(int(nbytes), 64), hipHostMallocMapped | hipHostMallocCoherent)
         if rc != 0:
             raise RuntimeError(f"hipHostMalloc({nbytes}) failed ({rc})")
         dp = ctypes.c_void_p()

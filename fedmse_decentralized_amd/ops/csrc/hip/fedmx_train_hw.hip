@@ -54,6 +54,13 @@
 #ifndef FEDMX_HW_FLAGS
 #define FEDMX_HW_FLAGS 0
 #endif
+// 1 (without FedProx): W1's Adam and the next layer-1 product software-
+// pipelined per half of the register tile: Adam of the v = 0 quads, their
+// layer-1 MFMAs, whose issue the v = 1 quads' Adam VALU then fills
+// (same per-accumulator order: bit-identical)
+#ifndef FEDMX_HW_PIPE
+#define FEDMX_HW_PIPE 0
+#endif
 // bound on one flag wait (polls); a wait that runs out marks the launch failed
 // (epochs_run = -1000) instead of hanging the GPU
 constexpr int HW_SPIN_LIMIT = 1 << 22;
@@ -923,12 +930,20 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
       HSTAMP(ms, 8);
       // ---- dW1^T (own columns) = X^T dH1
+      constexpr bool PIPE = FEDMX_HW_PIPE && !PROX;
 #pragma unroll
       for (int s = 0; s < KB; ++s) {
-        G1[0][0] = mfma16(cur.b0[s], dh1b[0][s], G1[0][0]);
-        G1[0][1] = mfma16(cur.b1[s], dh1b[0][s], G1[0][1]);
-        G1[1][0] = mfma16(cur.b0[s], dh1b[1][s], G1[1][0]);
-        G1[1][1] = mfma16(cur.b1[s], dh1b[1][s], G1[1][1]);
+        if (PIPE) {   // the v = 0 quads' gradients complete first
+          G1[0][0] = mfma16(cur.b0[s], dh1b[0][s], G1[0][0]);
+          G1[1][0] = mfma16(cur.b0[s], dh1b[1][s], G1[1][0]);
+          G1[0][1] = mfma16(cur.b1[s], dh1b[0][s], G1[0][1]);
+          G1[1][1] = mfma16(cur.b1[s], dh1b[1][s], G1[1][1]);
+        } else {
+          G1[0][0] = mfma16(cur.b0[s], dh1b[0][s], G1[0][0]);
+          G1[0][1] = mfma16(cur.b1[s], dh1b[0][s], G1[0][1]);
+          G1[1][0] = mfma16(cur.b0[s], dh1b[1][s], G1[1][0]);
+          G1[1][1] = mfma16(cur.b1[s], dh1b[1][s], G1[1][1]);
+        }
       }
       wave_sync();
       // ---- owned small tile: w<2 -> dW3 tile = dH3^T Z ; w>=2 -> dW2 tile = dZ^T H1
@@ -940,24 +955,47 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         for (int s = 0; s < KB; ++s) Go = mfma16(a[s], b[s], Go);
       }
       HSTAMP(ms, 9);
-      // W1 first: the next chunk's layer-1 product waits on it
+      auto adam_w1 = [&](int t, int v) {
+        if (FEDMX_HW_ABLATE & 32) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int v = 0; v < 2; ++v) {
-          if (FEDMX_HW_ABLATE & 32) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) P.q1[t][v][r] = __builtin_fmaf(G1[t][v][r], 0.f, P.q1[t][v][r]);
-          } else if (FEDMX_HW_PACKED && !PROX) {
-            adam4_packed(P.q1[t][v], M.q1[t][v], V.q1[t][v], G1[t][v], K);
-          } else {
-            adam4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
-          }
+          for (int r = 0; r < 4; ++r) P.q1[t][v][r] = __builtin_fmaf(G1[t][v][r], 0.f, P.q1[t][v][r]);
+        } else if (FEDMX_HW_PACKED && !PROX) {
+          adam4_packed(P.q1[t][v], M.q1[t][v], V.q1[t][v], G1[t][v], K);
+        } else {
+          adam4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
         }
-      HSTAMP(ms, 10);
-      // (after an epoch's last batch this works on a stale tile; unused)
-      finalize_chunk(nxt);
-      l1_partial(nxt, l1a, l1b);
+      };
+      if (PIPE) {
+        // Adam(v = 0 quads) -> their 8 layer-1 MFMAs, with Adam(v = 1 quads)
+        // issued between them -> the remaining 8 MFMAs
+        finalize_chunk(nxt);
+        adam_w1(0, 0);
+        adam_w1(1, 0);
+        l1a = zero4();
+        l1b = zero4();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          l1a = mfma16(P.q1[0][0][j], nxt.f0[j], l1a);
+          l1b = mfma16(P.q1[1][0][j], nxt.f0[j], l1b);
+        }
+        adam_w1(0, 1);
+        adam_w1(1, 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          l1a = mfma16(P.q1[0][1][j], nxt.f1[j], l1a);
+          l1b = mfma16(P.q1[1][1][j], nxt.f1[j], l1b);
+        }
+      } else {
+        // W1 first: the next chunk's layer-1 product waits on it
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int v = 0; v < 2; ++v) adam_w1(t, v);
+        HSTAMP(ms, 10);
+        // (after an epoch's last batch this works on a stale tile; unused)
+        finalize_chunk(nxt);
+        l1_partial(nxt, l1a, l1b);
+      }
       if (!(FEDMX_HW_ABLATE & 4)) {
         if (FEDMX_HW_PACKED && !PROX)
           adam4_packed(P.o, M.o, V.o, Go, K);

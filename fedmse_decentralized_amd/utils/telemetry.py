@@ -65,14 +65,18 @@ class Telemetry:
         try:
             yield
         finally:
-            if self.sync and self.sync_fn is not None:
-                self.sync_fn()
-            dt = time.perf_counter() - t0
-            self._stack.pop()
-            if self._stack:
-                self._stack[-1][0] += dt
-            if self.roctx is not None:
-                self.roctx.roctxRangePop()
+            try:
+                if self.sync and self.sync_fn is not None:
+                    self.sync_fn()   # may raise (a device error surfacing under --trace)
+            finally:
+                # the frame and the roctx range are closed whatever the sync did,
+                # so later phases never charge a dead parent
+                dt = time.perf_counter() - t0
+                self._stack.pop()
+                if self._stack:
+                    self._stack[-1][0] += dt
+                if self.roctx is not None:
+                    self.roctx.roctxRangePop()
             ex = dt - frame[0]
             self.round_times[name] += ex
             self.total[name] += ex

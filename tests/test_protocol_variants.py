@@ -201,3 +201,32 @@ def test_host_noise_rand_n_matches_scalar_draws():
     seq = [a.rand() for _ in range(40 * 39)] + [a.rand()]
     vec = list(b.rand_n(40 * 39)) + [b.rand()]
     assert seq == vec
+
+
+def test_fusion_weights_engine_forms_agree(tmp_path):
+    """the HIP engine forms fusion_avg weights with the torch
+    KDE / JS path (``Federation._fusion_weights_t``), the torch engine with
+    sklearn / scipy (``_fusion_similarity_of`` + ``fusion_weights``).  On
+    the same stacked models both must give the same weights (float64 on both
+    sides; stated tolerance rtol 1e-9), so the two engines stay comparable.
+    No reference fixture covers fusion_avg (parity unpinned vs the deleted
+    GlobalAggregator.fusion_avg)."""
+    import torch
+
+    from fedmse_decentralized_amd.config import ExperimentConfig
+    from fedmse_decentralized_amd.federation import Federation
+    from fedmse_decentralized_amd.utils.similarity import fusion_weights
+
+    cfg = ExperimentConfig(synthetic="nbaiot", network_size=4, num_rounds=1, epoch=1, compat="fixed", backend="torch",
+                           device="cpu", output_root=str(tmp_path), save_checkpoints=False, log_level="WARNING",
+                           global_early_stop=False, model_types=["hybrid"], update_types=["fusion_avg"],
+                           fusion_max_rows=256, init_mode="per_client")
+    fed = Federation(cfg, "hybrid", "fusion_avg", 0, write_reports=False).setup()
+    ids = [0, 1, 2, 3]
+    # distinct models: the per-client initial models, scaled differently
+    stack = fed.engine.store.params[ids].clone() * torch.tensor([1.0, 2.0, 0.5, 3.0])[:, None]
+    w_t = fed._fusion_weights_t(stack).cpu().numpy()
+    sim = fed._fusion_similarity_of(stack, ids)
+    w_h = fusion_weights([sim[c] for c in ids])
+    np.testing.assert_allclose(w_t, w_h, rtol=1e-9, atol=0)
+    assert abs(w_t.sum() - 1.0) < 1e-12 and len(set(np.round(w_t, 12))) > 1
