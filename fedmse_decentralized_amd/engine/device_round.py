@@ -175,7 +175,7 @@ class DeviceRound:
         numel = st.best.numel()
         self.snap_buf = _hip._hiprt.MappedBuffer(self.n_snap * numel * 4)
         C = st.best.shape[0]
-        self.snap_views = [torch.from_numpy(self.snap_buf.view(i * numel * 4, np.float32, numel).reshape(C, -1))
+        self.snap_views = [torch.from_numpy(self.snap_buf.view(i * numel * 4, np.float32, numel).reshape(C, P_PAD))
                            for i in range(self.n_snap)]
         # native checkpoint writer ticket of the job reading each slot (0: free)
         self.snap_ticket = [0] * self.n_snap

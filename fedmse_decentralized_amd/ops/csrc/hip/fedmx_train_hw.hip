@@ -51,6 +51,9 @@
 // waits on right before layer 4, instead of through barrier #1.  The
 // helpers then no longer gate the mains' layer-1 exchange: their W4 gradient
 // + Adam window runs from barrier #2 of step s to layer 4 of step s+1.
+// 2: barrier #2 as well: the mains exchange their dH3 partials through LDS
+// flags and each helper starts on its main's dY^T / H3^T as soon as that
+// main has written them (no workgroup barrier left in the step loop).
 #ifndef FEDMX_HW_FLAGS
 #define FEDMX_HW_FLAGS 0
 #endif
@@ -64,6 +67,7 @@
 // bound on one flag wait (polls); a wait that runs out marks the launch failed
 // (epochs_run = -1000) instead of hanging the GPU
 constexpr int HW_SPIN_LIMIT = 1 << 22;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 // (Round 3 also measured, and removed, seven schedule variants of this step --
 // dH3 partial reads in flight together, the bias column by address select,
 // helper-formed next-step Adam scalars, a software-pipelined tail, helper
@@ -202,17 +206,25 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // [neg_step_size, inv_bc2s, bc2s, -]; FEDMX_HW_FLAGS: one pair per helper
   float* const sK = reinterpret_cast<float*>(sLoss + 32);
   // FEDMX_HW_FLAGS: [0..3] layer-1 partials of step count v written by main w;
-  // [4..7] W4 / Adam scalars for step count v published by helper w
+  // [4..7] W4 / Adam scalars for step count v published by helper w;
+  // [8..11] (FLAGS 2) dH3 partial + dY^T / H3^T of step count v written by main w
   int* const sFlag = reinterpret_cast<int*>(sK + 32);
   bool spin_fail = false;
   auto flag_set = [&](int i, int v) {
     if (lane == 0) __hip_atomic_store(sFlag + i, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
+  // n = 4: one 16-byte volatile LDS read polls four flags (one round trip; four
+  // acquire loads would each wait for the previous one), then one acquire fence
   auto flag_wait = [&](int i0, int n, int v) {
     for (int it = 0;; ++it) {
-      int m = __hip_atomic_load(sFlag + i0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      for (int j = 1; j < n; ++j)
-        m = min(m, __hip_atomic_load(sFlag + i0 + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+      int m;
+      // (explicit LDS address space: a generic volatile pointer becomes a flat load)
+      if (n == 4) {
+        const i32x4 q = *(const volatile __attribute__((address_space(3))) i32x4*)(sFlag + i0);
+        m = min(min(q[0], q[1]), min(q[2], q[3]));
+      } else {
+        m = *(const volatile __attribute__((address_space(3))) int*)(sFlag + i0);
+      }
       if (m >= v) break;
       if (it >= HW_SPIN_LIMIT) {
         spin_fail = true;
@@ -220,6 +232,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
       __builtin_amdgcn_s_sleep(1);
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
 
   Lane L;
@@ -524,7 +537,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // (m, v, [anchor], params) in one memory round trip, then each tensor
   // passes through the masters in turn (the barrier sequence of one global_to_masters_o pass per tensor)
   HSTAMP(true, 28);
-  if (FEDMX_HW_FLAGS && threadIdx.x < 8) sFlag[threadIdx.x] = 0;   // (the staging barriers follow)
+  if (FEDMX_HW_FLAGS && threadIdx.x < 12) sFlag[threadIdx.x] = 0;   // (the staging barriers follow)
   f32x4 pv_m[STAGE_PER_THREAD], pv_v[STAGE_PER_THREAD], pv_a[STAGE_PER_THREAD], pv_p[STAGE_PER_THREAD];
   if (stager) {
     stage_load(Mg, pv_m);
@@ -583,7 +596,10 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         HSTAMP(hs, 0);
         if (!FEDMX_HW_FLAGS) __syncthreads();   // barrier #1 (main: layer-1 partials)
         HSTAMP(hs, 2);
-        __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
+        if (FEDMX_HW_FLAGS >= 2)
+          flag_wait(8 + w, 1, js + 1);   // main w's dY^T / H3^T of this step
+        else
+          __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
         HSTAMP(hs, 7);
         if (FEDMX_HW_ABLATE & 64) {
           ++js;
@@ -885,7 +901,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         sZT[tw + r * S_T] = zb[r];
       }
       HSTAMP(ms, 4);
-      __syncthreads();  // barrier #2: dH3 partials of all waves visible
+      if (FEDMX_HW_FLAGS >= 2) {
+        flag_set(8 + w, js);        // js = this step's count + 1 (incremented before layer 4)
+        flag_wait(8, 4, js);        // every main wave's dH3 partial of this step
+      } else {
+        __syncthreads();  // barrier #2: dH3 partials of all waves visible
+      }
       HSTAMP(ms, 7);
       f32x4 dh3[2];
 #pragma unroll

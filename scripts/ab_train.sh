@@ -8,7 +8,7 @@ cd "$ROOT"
 OUT=$ROOT/gpurun_out/ab
 mkdir -p "$OUT"
 LIBS=$(ls fedmse_decentralized_amd/ops/lib/libfedmx_hip_*.so | grep -v stamps)
-for rep in 1 2 3; do
+for rep in $(seq 1 ${AB_REPS:-3}); do
   for lib in $LIBS; do
     name=$(basename "$lib" .so)
     FEDMX_HIP_LIB=$ROOT/$lib timeout -k 10 120 python scripts/bench_kernels.py --train-only --reps 15 \

@@ -27,7 +27,9 @@ VARIANTS = {
     "flags_madam": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=32"],   # timing only: + mains skip W1 Adam
     "flags_hnone": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=64"],   # timing only: + helpers idle
     "pipe": ["-DFEDMX_HW_PIPE=1"],                   # r4: W1 Adam / next layer-1 software-pipelined by half-tile
-    "flags_pipe": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_PIPE=1"],                # r4: IEEE sqrt / division Adam (torch's op sequence)
+    "flags_pipe": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_PIPE=1"],
+    "flags2": ["-DFEDMX_HW_FLAGS=2"],                # r4: no workgroup barrier in the step loop
+    "flags2_pipe": ["-DFEDMX_HW_FLAGS=2", "-DFEDMX_HW_PIPE=1"],                # r4: IEEE sqrt / division Adam (torch's op sequence)
     "packed": ["-DFEDMX_HW_PACKED=1"],               # packed-fp32 Adam (bit-identical)  966-974 vs 948-951 (+2 %)
     "abl_pf": ["-DFEDMX_HW_ABLATE=8"],               # timing only: prefetch always hits the cache
     "abl_hadam": ["-DFEDMX_HW_ABLATE=16"],           # timing only: helpers skip W4's Adam
