@@ -66,7 +66,9 @@
 #endif
 // bound on one flag wait (polls); a wait that runs out marks the launch failed
 // (epochs_run = -1000) instead of hanging the GPU
-constexpr int HW_SPIN_LIMIT = 1 << 22;
+// (~1 ms of polls, vs ~3 us for a whole training step; after one wait has run
+// out the wave waits no more, so a broken hand-off ends the launch quickly)
+constexpr int HW_SPIN_LIMIT = 1 << 16;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 // (Round 3 also measured, and removed, seven schedule variants of this step --
 // dH3 partial reads in flight together, the bias column by address select,
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // n = 4: one 16-byte volatile LDS read polls four flags (one round trip; four
   // acquire loads would each wait for the previous one), then one acquire fence
   auto flag_wait = [&](int i0, int n, int v) {
-    for (int it = 0;; ++it) {
+    for (int it = 0; !spin_fail; ++it) {
       int m;
       // (explicit LDS address space: a generic volatile pointer becomes a flat load)
       if (n == 4) {
