@@ -668,7 +668,9 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
   }
   // ---- adoption + history + snapshots in one pass over the row
   if (FEDMX_VERIFY_ABLATE & 4) return;
-  const bool receiver = a >= 0 && c != a && A.mode == 0;
+  // (ModelVerifier receivers, absolute or relative drift limit: the history
+  // becomes the received aggregate whatever the decision)
+  const bool receiver = a >= 0 && c != a && (A.mode == 0 || A.mode == 3);
   constexpr int UA = (P_PAD / 4 + 511) / 512;   // every element of the row in one pass of loads
   f32x4 v[UA], pv[UA];
 #pragma unroll

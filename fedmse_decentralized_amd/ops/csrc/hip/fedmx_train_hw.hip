@@ -57,6 +57,12 @@
 #ifndef FEDMX_HW_FLAGS
 #define FEDMX_HW_FLAGS 0
 #endif
+// the same switch for the FedProx instantiation: 1 there (r4 A/B: FedProx
+// launch -3.3 %, the plain launch +6 % -- without FedProx the helpers' path is
+// short enough that the flag polls only add latency to the mains')
+#ifndef FEDMX_HW_FLAGS_PROX
+#define FEDMX_HW_FLAGS_PROX 1
+#endif
 // 1 (without FedProx): W1's Adam and the next layer-1 product software-
 // pipelined per half of the register tile: Adam of the v = 0 quads, their
 // layer-1 MFMAs, whose issue the v = 1 quads' Adam VALU then fills
@@ -178,6 +184,8 @@ struct XChunk {
 
 template <bool PROX>
 __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
+  // the flag hand-offs measured faster with FedProx only (profiles/r4_train_hw_experiments.md)
+  constexpr int HWF = PROX ? FEDMX_HW_FLAGS_PROX : FEDMX_HW_FLAGS;
   constexpr bool CP = true;
   constexpr int KB = 3;   // k-steps of products over the batch (compact order)
   constexpr int KZ = 2;   // k-steps of products over the latent axis
@@ -205,9 +213,9 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   float* const sQ4 = sRedDH3 + L_RED + 4 * L_SCR;   // [w][v][t][lane][4]
   double* const sLoss = reinterpret_cast<double*>(sQ4 + L_Q4);  // [8 waves][4]
   // per-step Adam scalars (helper -> main), double-buffered by step parity:
-  // [neg_step_size, inv_bc2s, bc2s, -]; FEDMX_HW_FLAGS: one pair per helper
+  // [neg_step_size, inv_bc2s, bc2s, -]; HWF: one pair per helper
   float* const sK = reinterpret_cast<float*>(sLoss + 32);
-  // FEDMX_HW_FLAGS: [0..3] layer-1 partials of step count v written by main w;
+  // HWF: [0..3] layer-1 partials of step count v written by main w;
   // [4..7] W4 / Adam scalars for step count v published by helper w;
   // [8..11] (FLAGS 2) dH3 partial + dY^T / H3^T of step count v written by main w
   int* const sFlag = reinterpret_cast<int*>(sK + 32);
@@ -539,7 +547,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // (m, v, [anchor], params) in one memory round trip, then each tensor
   // passes through the masters in turn (the barrier sequence of one global_to_masters_o pass per tensor)
   HSTAMP(true, 28);
-  if (FEDMX_HW_FLAGS && threadIdx.x < 12) sFlag[threadIdx.x] = 0;   // (the staging barriers follow)
+  if (HWF && threadIdx.x < 12) sFlag[threadIdx.x] = 0;   // (the staging barriers follow)
   f32x4 pv_m[STAGE_PER_THREAD], pv_v[STAGE_PER_THREAD], pv_a[STAGE_PER_THREAD], pv_p[STAGE_PER_THREAD];
   if (stager) {
     stage_load(Mg, pv_m);
@@ -582,23 +590,23 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     int js = 0;   // step index within the launch
     auto publish_k = [&]() {
       next_constants();
-      if (FEDMX_HW_FLAGS) {
+      if (HWF) {
         if (lane == 0) lds_write4(sK + 8 * w + 4 * (js & 1), f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f});
       } else if (lane == 0 && w8 == 4) {
         lds_write4(sK + 4 * (js & 1), f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f});
       }
     };
     publish_k();   // step 0's
-    if (FEDMX_HW_FLAGS) flag_set(4 + w, 1);   // W4 / scalars of launch step 0 published
+    if (HWF) flag_set(4 + w, 1);   // W4 / scalars of launch step 0 published
     for (int ep = 0; ep < A.epochs; ++ep) {
       double acc_tr = 0.0;
       // W4 gradient + Adam between barrier #2 of step s and barrier #1 of s+1
       for (int bi = 0; bi < nb; ++bi) {
         const bool hs = (ep == 0 && bi == STAMP_STEP);
         HSTAMP(hs, 0);
-        if (!FEDMX_HW_FLAGS) __syncthreads();   // barrier #1 (main: layer-1 partials)
+        if (!HWF) __syncthreads();   // barrier #1 (main: layer-1 partials)
         HSTAMP(hs, 2);
-        if (FEDMX_HW_FLAGS >= 2)
+        if (HWF >= 2)
           flag_wait(8 + w, 1, js + 1);   // main w's dY^T / H3^T of this step
         else
           __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
@@ -606,7 +614,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         if (FEDMX_HW_ABLATE & 64) {
           ++js;
           publish_k();
-          if (FEDMX_HW_FLAGS) flag_set(4 + w, js + 1);
+          if (HWF) flag_set(4 + w, js + 1);
           continue;
         }
         const f32x4 w4a0 = lds_read4(sT0 + tr);
@@ -648,7 +656,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         publish_q4();
         ++js;
         publish_k();   // step js's scalars, read by the mains after its barrier #1
-        if (FEDMX_HW_FLAGS) flag_set(4 + w, js + 1);   // W4(js) ready for main w's layer 4
+        if (HWF) flag_set(4 + w, js + 1);   // W4(js) ready for main w's layer 4
         HSTAMP(hs, 11);
       }
       double prox_now = 0.0;
@@ -753,7 +761,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         lds_write4(red + (w * 2 + 0) * 256 + lane * 4, l1a);
         lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1b);
         HSTAMP(ms, 1);
-        if (FEDMX_HW_FLAGS) {
+        if (HWF) {
           flag_set(w, js + 1);        // (release: the partial writes above complete first)
           flag_wait(0, 4, js + 1);    // every main wave's partial of this step
         } else {
@@ -762,7 +770,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         HSTAMP(ms, 2);
         auto read_helper_state = [&]() {
           // this step's Adam scalars (helper-published)
-          const f32x4 kk = lds_read4(FEDMX_HW_FLAGS ? sK + 8 * w + 4 * (js & 1) : sK + 4 * (js & 1));
+          const f32x4 kk = lds_read4(HWF ? sK + 8 * w + 4 * (js & 1) : sK + 4 * (js & 1));
           K.neg_step_size = kk[0];
           K.inv_bc2s = kk[1];
           K.bc2s = kk[2];
@@ -772,7 +780,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
             for (int t = 0; t < 2; ++t) q4[v][t] = lds_read4(q4p + (2 * v + t) * 256);
         };
-        if (!FEDMX_HW_FLAGS) read_helper_state();
+        if (!HWF) read_helper_state();
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           f32x4 s = lds_read4(red + t * 256 + lane * 4);
@@ -816,7 +824,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           h3[0] = acc0;
           h3[1] = acc1;
         }
-        if (FEDMX_HW_FLAGS) {
+        if (HWF) {
           flag_wait(4 + w, 1, js + 1);   // helper w has published W4(s) and the scalars
           read_helper_state();
         }
@@ -903,7 +911,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         sZT[tw + r * S_T] = zb[r];
       }
       HSTAMP(ms, 4);
-      if (FEDMX_HW_FLAGS >= 2) {
+      if (HWF >= 2) {
         flag_set(8 + w, js);        // js = this step's count + 1 (incremented before layer 4)
         flag_wait(8, 4, js);        // every main wave's dH3 partial of this step
       } else {
@@ -1074,7 +1082,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     A.epochs_run[kslot] = ep_run;
     A.best_epoch[kslot] = best_ep;
   }
-  if (FEDMX_HW_FLAGS && spin_fail && lane == 0) A.epochs_run[kslot] = -1000;   // a flag wait ran out
+  if (HWF && spin_fail && lane == 0) A.epochs_run[kslot] = -1000;   // a flag wait ran out
 }
 
 }  // namespace hw
