@@ -4,12 +4,15 @@
 #pragma once
 #include "fedmx_common.h"
 
+// 1: IEEE square root and divisions in the Adam denominator / quotient
+// (adam4) instead of the hardware v_sqrt_f32 / v_rcp_f32
 #ifndef FEDMX_EXACT_ADAM
 #define FEDMX_EXACT_ADAM 0
 #endif
-// 1: fused multiply-adds in the Adam update (fewer VALU issues on the
-// optimizer-bound tail of the step, -2% launch time measured); 0: separately
-// rounded multiply / add as the torch op sequence
+// 1: fused multiply-adds in the Adam update where torch's CPU vector kernels
+// fuse (lerp, addcmul, addcdiv; also fewer VALU issues on the optimizer-bound
+// tail of the step, -2% launch time measured); 0: every multiply and add
+// separately rounded
 #ifndef FEDMX_ADAM_FMA
 #define FEDMX_ADAM_FMA 1
 #endif
@@ -110,40 +113,20 @@ __device__ __forceinline__ void adam4s(float (&p)[4], float (&m)[4], float (&v)[
 // torch.optim.Adam single-tensor update (no weight decay / amsgrad):
 //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2)
 //   p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1)
-// Default build: hardware sqrt / reciprocal (<= 1 ulp each) instead of the
-// IEEE division sequences — 4x fewer instructions on the critical path.
-template <bool PROX>
-__device__ __forceinline__ void adam_update(float& p, float& m, float& v, float a, float grad, const AdamStep& K,
-                                            float& prox_acc) {
-  float gr = grad;
-  if (PROX) {
-    const float dp = p - a;
-    prox_acc += dp * dp;
-    gr = gr + K.two_mu * dp;
-  }
-  m = m + K.one_m_b1 * (gr - m);
-  v = v * K.b2 + (K.one_m_b2 * gr) * gr;
-#if FEDMX_EXACT_ADAM
-  const float den = __fsqrt_rn(v) / K.bc2s + K.eps;
-  p = p + K.neg_step_size * (m / den);
-#else
-  const float den = __builtin_amdgcn_sqrtf(v) * K.inv_bc2s + K.eps;
-  p = p + K.neg_step_size * (m * __builtin_amdgcn_rcpf(den));
-#endif
-}
-
+// in the fused form torch's CPU vector kernels use (lerp, addcmul and addcdiv
+// as fused multiply-adds: the oracle test over 5,700 steps agrees to 6e-8 in
+// the parameters, tests/test_long_horizon_gpu.py).  Default build: hardware
+// square root and reciprocal (<= 1 ulp each) for sqrt(v) / sqrt(bc2) and the
+// division; FEDMX_EXACT_ADAM=1: IEEE square root and divisions there (54 %
+// slower launch, profiles/r4_train_hw_experiments.md).
 // Four elements (one accumulator register quad) at a time, stage-major: every
 // stage issues four independent scalar ops, so consecutive VALU instructions
 // never depend on each other (no hazard s_nops between dependent packed ops,
 // which the packed-fp32 form paid on gfx950) and the scheduler can slot them
-// into MFMA gaps.  Same operation order per element as adam_update.
+// into MFMA gaps.
 template <bool PROX>
 __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4], const float (&a)[4], f32x4 g,
                                       const AdamStep& K, float& prox_acc) {
-#if FEDMX_EXACT_ADAM
-#pragma unroll
-  for (int r = 0; r < 4; ++r) adam_update<PROX>(p[r], m[r], v[r], a[r], g[r], K, prox_acc);
-#else
   float gr[4], t0[4], t1[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) gr[r] = g[r];
@@ -169,6 +152,14 @@ __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4
   for (int r = 0; r < 4; ++r) t1[r] = K.one_m_b2 * gr[r];
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(t1[r], gr[r], t0[r]);
+#if FEDMX_EXACT_ADAM
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t0[r] = __fsqrt_rn(v[r]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t0[r] = t0[r] / K.bc2s + K.eps;   // (-ffp-contract=off: two roundings)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t1[r] = m[r] / t0[r];
+#else
 #pragma unroll
   for (int r = 0; r < 4; ++r) t0[r] = __builtin_amdgcn_sqrtf(v[r]);
 #pragma unroll
@@ -177,6 +168,7 @@ __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4
   for (int r = 0; r < 4; ++r) t1[r] = __builtin_amdgcn_rcpf(t0[r]);
 #pragma unroll
   for (int r = 0; r < 4; ++r) t1[r] = m[r] * t1[r];
+#endif
 #pragma unroll
   for (int r = 0; r < 4; ++r) p[r] = __builtin_fmaf(K.neg_step_size, t1[r], p[r]);
 #else
@@ -200,7 +192,6 @@ __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4
   for (int r = 0; r < 4; ++r) t1[r] = m[r] * t1[r];
 #pragma unroll
   for (int r = 0; r < 4; ++r) p[r] = p[r] + K.neg_step_size * t1[r];
-#endif
 #endif
 }
 
