@@ -28,6 +28,7 @@ VARIANTS = {
     "flags_hnone": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=64"],   # timing only: + helpers idle
     "pipe": ["-DFEDMX_HW_PIPE=1"],                   # r4: W1 Adam / next layer-1 software-pipelined by half-tile
     "flags_pipe": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_PIPE=1"],
+    "split": ["-DFEDMX_HW_SPLIT=1"],                 # r4: layer-1 hidden tile 1 + its backward / Adam on the helpers
     "flags2": ["-DFEDMX_HW_FLAGS=2"],                # r4: no workgroup barrier in the step loop
     "flags2_pipe": ["-DFEDMX_HW_FLAGS=2", "-DFEDMX_HW_PIPE=1"],                # r4: IEEE sqrt / division Adam (torch's op sequence)
     "packed": ["-DFEDMX_HW_PACKED=1"],               # packed-fp32 Adam (bit-identical)  966-974 vs 948-951 (+2 %)
