@@ -79,8 +79,18 @@
 // backward -> Adam -> layer-1 chain instead of the main wave running it
 // alone.  The helpers' W4 Adam moves behind barrier #1 (it overlaps the
 // mains' layers 2-3) and is handed to the mains' layer 4 through an LDS flag.
+#ifndef FEDMX_HW_RED8
+#define FEDMX_HW_RED8 0   // (experiment) the eight dH3 partial reads after barrier #2 issued together
+#endif
 #ifndef FEDMX_HW_SPLIT
 #define FEDMX_HW_SPLIT 0
+#endif
+// debug bits for SPLIT (diagnosis builds only): 1 = the mains also form
+// layer 1's hidden tile 1 and write it instead of the helpers; 2 = the mains
+// also form it, and both roles dump their tile-1 partial of the launch's first
+// step (workgroup 0) into A.stamps (mains [0, 1024), helpers [1024, 2048))
+#ifndef FEDMX_HW_SPLIT_DEBUG
+#define FEDMX_HW_SPLIT_DEBUG 0
 #endif
 // bound on one flag wait (polls); a wait that runs out marks the launch failed
 // (epochs_run = -1000) instead of hanging the GPU
@@ -654,9 +664,24 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         const bool has_next = bi + 1 < nb;
         const int bt = has_next ? B : bt_last_h;
         float* red = sRedH1 + parity * L_RED;
-        lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1h);   // this wave's half of the layer-1 partial
+        if ((FEDMX_HW_SPLIT_DEBUG & 2) && ep == 0 && bi == 0 && blockIdx.x == 0 && A.stamps != nullptr) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) A.stamps[1024 + (w * 64 + lane) * 4 + r] = (uint64_t)__float_as_uint(l1h[r]);
+        }
+        if (!(FEDMX_HW_SPLIT_DEBUG & 1))
+          lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1h);   // this wave's half of the layer-1 partial
         __syncthreads();   // barrier #1
         parity ^= 1;
+        // W3 / W2 columns of this step: read now, while the masters hold W(s)
+        // (mains 0-3 publish W(s+1) at the end of their segment B, before this
+        // wave's dZ / dH1 below)
+        float q3h[2][4], q2h[4];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) q3h[t][r] = d3p[(16 * t + r) * S_W3];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q2h[r] = d2p[r * S_W2 + 16];
         if (g4_pending) apply_w4();
         __syncthreads();   // barrier #2 (main: dY^T / H3^T / dH3 partials / H1^T / Z^T written)
         // ---- dW4 (own rows) of this step
@@ -697,11 +722,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           }
           dh3[t] = sm;
         }
-        float q3h[2][4], zh[4];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) q3h[t][r] = d3p[(16 * t + r) * S_W3];
+        float zh[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) zh[r] = sZT[tw + r * S_T];
         float nz = 0.f;
@@ -720,9 +741,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         f32x4 dh1;
         {
           const f32x4 h1b1 = lds_read4(sH1T + tr + 16 * S_T);
-          float q2h[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) q2h[r] = d2p[r * S_W2 + 16];
           f32x4 acc = zero4();
 #pragma unroll
           for (int s2 = 0; s2 < KZ; ++s2) acc = mfma16(dz[s2], q2h[s2], acc);
@@ -912,7 +930,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   auto l1_partial = [&](const XChunk& x, f32x4& acc0, f32x4& acc1) {
     acc0 = zero4();
     acc1 = zero4();
-    if (SPL) {   // hidden tile 1 is the helper's
+    if (SPL && !(FEDMX_HW_SPLIT_DEBUG & 3)) {   // hidden tile 1 is the helper's
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc0 = mfma16(P.q1[0][0][j], x.f0[j], acc0);
 #pragma unroll
@@ -970,7 +988,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       {
         float* red = sRedH1 + parity * L_RED;
         lds_write4(red + (w * 2 + 0) * 256 + lane * 4, l1a);
-        if (!SPL) lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1b);   // SPLIT: the helper's slot
+        if ((FEDMX_HW_SPLIT_DEBUG & 2) && ep == 0 && bi == 0 && blockIdx.x == 0 && A.stamps != nullptr) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) A.stamps[(w * 64 + lane) * 4 + r] = (uint64_t)__float_as_uint(l1b[r]);
+        }
+        if (!SPL || (FEDMX_HW_SPLIT_DEBUG & 1))
+          lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1b);   // SPLIT: the helper's slot
         HSTAMP(ms, 1);
         if (HWF) {
           flag_set(w, js + 1);        // (release: the partial writes above complete first)
@@ -1130,12 +1153,19 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
       HSTAMP(ms, 7);
       f32x4 dh3[2];
+      f32x4 red8[2][4];
+      if (FEDMX_HW_RED8) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int ww = 0; ww < 4; ++ww) red8[t][ww] = lds_read4(sRedDH3 + (ww * 2 + t) * 256 + lane * 4);
+      }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        f32x4 s = lds_read4(sRedDH3 + t * 256 + lane * 4);
+        f32x4 s = FEDMX_HW_RED8 ? red8[t][0] : lds_read4(sRedDH3 + t * 256 + lane * 4);
 #pragma unroll
         for (int ww = 1; ww < 4; ++ww) {
-          const f32x4 o = lds_read4(sRedDH3 + (ww * 2 + t) * 256 + lane * 4);
+          const f32x4 o = FEDMX_HW_RED8 ? red8[t][ww] : lds_read4(sRedDH3 + (ww * 2 + t) * 256 + lane * 4);
 #pragma unroll
           for (int r = 0; r < 4; ++r) s[r] = s[r] + o[r];
         }

@@ -22,15 +22,18 @@ VARIANTS = {
     # helper delays hd8/16/24, priorities hprio1/3 and (r2) hwprio1/3: all measured slower or
     # neutral (profiles/r3_train_hw_experiments.md); their switches were removed from the kernel
     # (source in git history, commit 5365856)
-    "exact": ["-DFEDMX_EXACT_ADAM=1"],
+    "exact": ["-DFEDMX_EXACT_ADAM=1"],               # r4: IEEE sqrt / division Adam (torch's op sequence)
     "flags": ["-DFEDMX_HW_FLAGS=1"],                 # r4: mains-only layer-1 exchange + helper->main LDS flags
     "flags_madam": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=32"],   # timing only: + mains skip W1 Adam
     "flags_hnone": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=64"],   # timing only: + helpers idle
     "pipe": ["-DFEDMX_HW_PIPE=1"],                   # r4: W1 Adam / next layer-1 software-pipelined by half-tile
     "flags_pipe": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_PIPE=1"],
-    "split": ["-DFEDMX_HW_SPLIT=1"],                 # r4: layer-1 hidden tile 1 + its backward / Adam on the helpers
+    "hwsplit": ["-DFEDMX_HW_SPLIT=1"],               # r4: layer-1 hidden tile 1 + its backward / Adam on the helpers
+    "red8": ["-DFEDMX_HW_RED8=1"],                   # r4: dH3 partial reads issued together (the ISA co-simulation predicts -4.6 %)
+    "hwsplitd1": ["-DFEDMX_HW_SPLIT=1", "-DFEDMX_HW_SPLIT_DEBUG=1"],   # diagnosis only
+    "hwsplitd2": ["-DFEDMX_HW_SPLIT=1", "-DFEDMX_HW_SPLIT_DEBUG=2"],   # diagnosis only
     "flags2": ["-DFEDMX_HW_FLAGS=2"],                # r4: no workgroup barrier in the step loop
-    "flags2_pipe": ["-DFEDMX_HW_FLAGS=2", "-DFEDMX_HW_PIPE=1"],                # r4: IEEE sqrt / division Adam (torch's op sequence)
+    "flags2_pipe": ["-DFEDMX_HW_FLAGS=2", "-DFEDMX_HW_PIPE=1"],
     "packed": ["-DFEDMX_HW_PACKED=1"],               # packed-fp32 Adam (bit-identical)  966-974 vs 948-951 (+2 %)
     "abl_pf": ["-DFEDMX_HW_ABLATE=8"],               # timing only: prefetch always hits the cache
     "abl_hadam": ["-DFEDMX_HW_ABLATE=16"],           # timing only: helpers skip W4's Adam
@@ -41,7 +44,7 @@ VARIANTS = {
     "hint1": ["-DFEDMX_SCHED_HINTS=1"],           # 64 x (1 MFMA, 6 VALU)      (+9%)
     "sepadam": ["-DFEDMX_ADAM_FMA=0"],            # separately rounded Adam    (+3%)
     "dw4late": ["-DFEDMX_DW4_LATE=1"],            # dW4 products after barrier #2 (+0.5%)
-    "split": ["-DFEDMX_SPLIT_CHAINS=1"],          # L2 / dZ as two accumulator chains (+0.3%)
+    "split_chains": ["-DFEDMX_SPLIT_CHAINS=1"],   # 4-wave kernel: L2 / dZ as two accumulator chains (+0.3%)
     "novgprform": ["-mllvm", "-amdgpu-mfma-vgpr-form=0"],  # AGPR accumulators (+3.3%)
     "noslp": ["-fno-slp-vectorize"],              # no packed fp32 VALU        (+5%)
     "w4pos1": ["-DFEDMX_W4_POS=1"],               # W4 Adam after dH1, fenced   (+2.5%)

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round-4 GPU call A: MFMA chain probe, GPU test tier + bench + paper config,
+# then the kernel A/B (HW_SPLIT / RED8 bit-identity, train-launch timing).
+set -u
+mkdir -p gpurun_out/r4b
+timeout -k 10 60 scripts/probes/mfma_chain > gpurun_out/r4b/mfma_chain.json || { echo "probe rc=$?"; exit 1; }
+cat gpurun_out/r4b/mfma_chain.json
+bash scripts/r4_gpu_check.sh gpurun_out/r4b || exit 1
+AB_REPS=2 AB_CHECK="hwsplit red8" bash scripts/r4_ab.sh || exit 1

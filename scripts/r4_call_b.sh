@@ -1,8 +1,8 @@
 #!/bin/bash
-# GPU test tier + bench + paper config, the adoption ablation, a kernel-trace
-# profile of the bench; stops at the first failure.
+# Round-4 GPU call B: the adoption ablation (HIP engine) and a kernel-trace
+# profile of the headline bench.
 set -u
-bash scripts/r4_gpu_check.sh gpurun_out/r4b || exit 1
+mkdir -p gpurun_out/r4b
 bash scripts/r4_adoption.sh gpurun_out/r4_adoption || exit 1
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$OLDPWD}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4b/prof -o run -- python3 bench.py --steps 20 --warmup 3 \

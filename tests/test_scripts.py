@@ -197,3 +197,45 @@ def test_plots_scale_combos_and_tsne(tmp_path):
     assert os.path.getsize(out) > 1000
     out = plots.plot_combos(os.path.join(str(tmp_path), "Checkpoint/Results"), str(tmp_path / "combos.png"))
     assert os.path.getsize(out) > 1000
+
+
+def test_ab_variant_names_are_unique():
+    """A repeated key in scripts/ab_variants.py's table silently replaces the
+    earlier variant's flags (round 4: a second "split" entry built a 4-wave
+    kernel variant under the helper-wave SPLIT name)."""
+    import ast
+    import collections
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    tree = ast.parse(open(os.path.join(root, "scripts", "ab_variants.py")).read())
+    table = next(n.value for n in tree.body if isinstance(n, ast.Assign) and
+                 any(getattr(t, "id", None) == "VARIANTS" for t in n.targets))
+    keys = [k.value for k in table.keys]
+    assert [k for k, c in collections.Counter(keys).items() if c > 1] == []
+
+
+def test_isa_timeline_on_a_tiny_listing(tmp_path):
+    """scripts/isa_timeline.py: a dependent MFMA pair waits 40 cycles, an LDS
+    read's consumer waits for lgkmcnt; the loop / barrier plumbing runs."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    import isa_timeline as T
+
+    body = T.parse([
+        "\tds_read_b128 v[0:3], v10",
+        "\ts_waitcnt lgkmcnt(0)",
+        "\tv_mfma_f32_16x16x4_f32 v[4:7], v0, v1, v[4:7]",
+        "\tv_mfma_f32_16x16x4_f32 v[4:7], v2, v3, v[4:7]",
+        "\tv_add_f32_e32 v8, v4, v5",
+    ])
+    rows, t = T.simulate(body)
+    assert rows[1]["why"] == "lgkmcnt" and rows[1]["stall"] == T.LDS_LAT + T.LDS_B128 - 4
+    assert rows[3]["issue"] - rows[2]["issue"] == 40
+    assert rows[4]["issue"] - rows[3]["issue"] == 40
+    asm = "\n".join(["_Zk:", ".LBB0_1:", "\ts_barrier", "\tv_mfma_f32_16x16x4_f32 v[4:7], v0, v1, v[4:7]",
+                     "\ts_barrier", "\tv_add_f32_e32 v8, v4, v5", "\ts_cbranch_scc1 .LBB0_1", ".Lfunc_end0:"])
+    lines = asm.split("\n")
+    st, en = T.find_kernel(lines, "_Zk")
+    lp = T.loops(lines, st, en)
+    assert lp and lp[0]["mfma"] == 1 and lp[0]["barriers"] == 2
+    ws = T.cosim([T.parse(lines[lp[0]["start"]:lp[0]["end"] + 1])] * 2, ["a", "b"], iters=3)
+    assert all(w.iters == 3 for w in ws)
