@@ -113,12 +113,13 @@ __device__ __forceinline__ void adam4s(float (&p)[4], float (&m)[4], float (&v)[
 // torch.optim.Adam single-tensor update (no weight decay / amsgrad):
 //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2)
 //   p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1)
-// in the fused form torch's CPU vector kernels use (lerp, addcmul and addcdiv
-// as fused multiply-adds: the oracle test over 5,700 steps agrees to 6e-8 in
-// the parameters, tests/test_long_horizon_gpu.py).  Default build: hardware
-// square root and reciprocal (<= 1 ulp each) for sqrt(v) / sqrt(bc2) and the
-// division; FEDMX_EXACT_ADAM=1: IEEE square root and divisions there (54 %
-// slower launch, profiles/r4_train_hw_experiments.md).
+// Default build: lerp and addcmul fused as torch's CPU vector kernels fuse
+// them, the denominator and the update as two fused multiply-adds around the
+// hardware square root and reciprocal (<= 1 ulp each): over 5,700 steps at
+// the paper's hyper-parameters it agrees with the torch oracle to 6e-8 in the
+// parameters (tests/test_long_horizon_gpu.py).  FEDMX_EXACT_ADAM=1: torch's
+// exact rounding sequence with IEEE square root and divisions (54 % slower
+// launch, profiles/r4_train_hw_experiments.md).
 // Four elements (one accumulator register quad) at a time, stage-major: every
 // stage issues four independent scalar ops, so consecutive VALU instructions
 // never depend on each other (no hazard s_nops between dependent packed ops,
@@ -153,12 +154,21 @@ __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(t1[r], gr[r], t0[r]);
 #if FEDMX_EXACT_ADAM
+  // torch's CPU op sequence, rounding for rounding (checked against torch
+  // 2.10 on the CPU: lerp and addcmul fused, `(sqrt(v) / bc2s) + eps` and
+  // addcdiv's `p + (value * m) / denom` separately rounded); only torch's
+  // vectorised sqrt (SLEEF, 0.5001 ulp: ~0.6 % of inputs off by one ulp)
+  // differs from the IEEE square root used here
 #pragma unroll
   for (int r = 0; r < 4; ++r) t0[r] = __fsqrt_rn(v[r]);
 #pragma unroll
   for (int r = 0; r < 4; ++r) t0[r] = t0[r] / K.bc2s + K.eps;   // (-ffp-contract=off: two roundings)
 #pragma unroll
-  for (int r = 0; r < 4; ++r) t1[r] = m[r] / t0[r];
+  for (int r = 0; r < 4; ++r) t1[r] = K.neg_step_size * m[r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t1[r] = t1[r] / t0[r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p[r] = p[r] + t1[r];
 #else
 #pragma unroll
   for (int r = 0; r < 4; ++r) t0[r] = __builtin_amdgcn_sqrtf(v[r]);
@@ -168,9 +178,9 @@ __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4
   for (int r = 0; r < 4; ++r) t1[r] = __builtin_amdgcn_rcpf(t0[r]);
 #pragma unroll
   for (int r = 0; r < 4; ++r) t1[r] = m[r] * t1[r];
-#endif
 #pragma unroll
   for (int r = 0; r < 4; ++r) p[r] = __builtin_fmaf(K.neg_step_size, t1[r], p[r]);
+#endif
 #else
 #pragma unroll
   for (int r = 0; r < 4; ++r) t0[r] = gr[r] - m[r];

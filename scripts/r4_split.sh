@@ -1,7 +1,7 @@
 #!/bin/bash
 set -u
 mkdir -p gpurun_out/split
-for v in ${DIAG_LIBS:-split base}; do
+for v in ${DIAG_LIBS:-hwsplit base}; do
 FEDMX_HIP_LIB=$PWD/fedmse_decentralized_amd/ops/lib/libfedmx_hip_$v.so timeout -k 10 120 python scripts/r4_split_diag.py > gpurun_out/split/diag_$v.txt 2>&1; echo "diag $v rc=$?"; grep -v amdgpu.ids gpurun_out/split/diag_$v.txt | python -c "
 import sys, ast
 for l in sys.stdin:
