@@ -204,19 +204,11 @@ struct XChunk {
   f32x4 f0, f1, b0, b1;
 };
 
-// MULTI: batches of more than 12 rows (VERDICT r3 Next #7: the thesis's GPU
-// runs use batch 64).  A batch is a sequence of 12-row chunks in the same
-// compact order; every chunk runs the step's forward / backward with its two
-// barriers, the weight gradients accumulate over the batch's chunks, and
-// Adam (main W1 + small tiles, helper W4) and the W4 / scalar hand-off run
-// after the batch's last chunk only.  Loss and gradient scales use the
-// batch's row count, the column masks the chunk's.
-template <bool PROX, bool MULTI>
+template <bool PROX>
 __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // the flag hand-offs measured faster with FedProx only (profiles/r4_train_hw_experiments.md)
-  constexpr int HWF = MULTI ? 0 : (PROX ? FEDMX_HW_FLAGS_PROX : FEDMX_HW_FLAGS);
-  constexpr bool SPL = FEDMX_HW_SPLIT && !PROX && !HWF && !MULTI;
-  constexpr int CH = 12;   // MULTI: rows per chunk (the compact batch order's 12 columns)
+  constexpr int HWF = PROX ? FEDMX_HW_FLAGS_PROX : FEDMX_HW_FLAGS;
+  constexpr bool SPL = FEDMX_HW_SPLIT && !PROX && !HWF;
   constexpr bool W4FLAG = HWF || SPL;   // W4 / Adam scalars handed over by LDS flag (per-helper K slots)
   constexpr bool CP = true;
   constexpr int KB = 3;   // k-steps of products over the batch (compact order)
@@ -833,14 +825,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       // W4 gradient + Adam between barrier #2 of step s and barrier #1 of s+1
       for (int bi = 0; bi < nb; ++bi) {
         const bool hs = (ep == 0 && bi == STAMP_STEP);
-        // MULTI: the batch's chunks (barriers as the main waves'); dW4 accumulates
-        const int nch = MULTI ? (min(B, n_tr - bi * B) + CH - 1) / CH : 1;
-        f32x4 G4[2][2];
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-#pragma unroll
-          for (int t = 0; t < 2; ++t) G4[v][t] = zero4();
-        for (int ch = 0; ch < nch; ++ch) {
         HSTAMP(hs, 0);
         if (!HWF) __syncthreads();   // barrier #1 (main: layer-1 partials)
         HSTAMP(hs, 2);
@@ -849,24 +833,27 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         else
           __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
         HSTAMP(hs, 7);
-        if (FEDMX_HW_ABLATE & 64) continue;
+        if (FEDMX_HW_ABLATE & 64) {
+          ++js;
+          publish_k();
+          if (HWF) flag_set(4 + w, js + 1);
+          continue;
+        }
         const f32x4 w4a0 = lds_read4(sT0 + tr);
         const f32x4 w4a1 = lds_read4(sT0 + tr + 16 * S_T);
         const f32x4 w4b0 = lds_read4(sT1 + tr);
         const f32x4 w4b1 = lds_read4(sT1 + tr + 16 * S_T);
+        f32x4 G4[2][2];
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) G4[v][t] = zero4();
 #pragma unroll
         for (int s = 0; s < KB; ++s) {
           G4[0][0] = mfma16(w4a0[s], w4b0[s], G4[0][0]);
           G4[0][1] = mfma16(w4a0[s], w4b1[s], G4[0][1]);
           G4[1][0] = mfma16(w4a1[s], w4b0[s], G4[1][0]);
           G4[1][1] = mfma16(w4a1[s], w4b1[s], G4[1][1]);
-        }
-        }
-        if (FEDMX_HW_ABLATE & 64) {
-          ++js;
-          publish_k();
-          if (HWF) flag_set(4 + w, js + 1);
-          continue;
         }
         HSTAMP(hs, 8);
         float prox_acc = 0.f;
@@ -983,23 +970,17 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     for (int bi = 0; bi < nb; ++bi) {
       const int row_b = bi * B;
       const int bt = min(B, n_tr - row_b);
-      const bool has_next_b = bi + 1 < nb;
-      const float inv_bt = has_next_b ? inv_b_full : inv_b_last;
+      const bool has_next = bi + 1 < nb;
+      const int row_n = (bi + 1) * B;
+      const int bc_n = has_next ? min(B, n_tr - row_n) : 0;
+      const float inv_bt = has_next ? inv_b_full : inv_b_last;
       const bool ms = (ep == 0 && bi == STAMP_STEP);
+      HSTAMP(ms, 0);
       f32x4 G1[2][2], Go = zero4();
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int v = 0; v < 2; ++v) G1[t][v] = zero4();
-      // MULTI: the batch's 12-row chunks; otherwise one chunk = the batch
-      const int nch = MULTI ? (bt + CH - 1) / CH : 1;
-      for (int ch = 0; ch < nch; ++ch) {
-      const bool last_ch = !MULTI || ch + 1 == nch;   // Adam / hand-offs after the batch's last chunk
-      const int bc = MULTI ? min(CH, bt - CH * ch) : bt;   // rows of this chunk (column masks)
-      const bool has_next = MULTI ? (!last_ch || has_next_b) : has_next_b;   // a chunk to prefetch
-      const int row_n = MULTI ? (last_ch ? row_b + B : row_b + CH * (ch + 1)) : (bi + 1) * B;
-      const int bc_n = has_next ? min(B, n_tr - row_n) : 0;
-      HSTAMP(ms, 0);
 
       // ---- forward: layer-1 K reduction (barrier #1), layers 2-4, loss
       f32x4 h1[2], z, zb, h3[2], y[2], q4[2][2];
@@ -1081,7 +1062,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           flag_wait(4 + w, 1, js + 1);   // helper w has published W4(s) and the scalars
           read_helper_state();
         }
-        if (last_ch) ++js;
+        ++js;
         {
           f32x4 acc0 = zero4(), acc1 = zero4();
           const f32x4 a00 = lds_read4(a4p);
@@ -1108,7 +1089,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           const float d1 = (bias_lane && r == 3) ? 0.f : y[1][r] - cur.f1[r];
           sq += d0 * d0 + d1 * d1;
         }
-        const bool col_ok = (unsigned)brow_c < (unsigned)bc;
+        const bool col_ok = (unsigned)brow_c < (unsigned)bt;
         sq = col_ok ? sq : 0.f;
         float nz = 0.f;
 #pragma unroll
@@ -1132,8 +1113,8 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         }
 
       // ---- dY (masked, feature-major); dY^T / H3^T for the helper's dW4
-      const bool col_ok = (unsigned)brow_c < (unsigned)bc;
-      const float scale = col_ok ? (has_next_b ? scale_full : scale_last) : 0.f;
+      const bool col_ok = (unsigned)brow_c < (unsigned)bt;
+      const float scale = col_ok ? (has_next ? scale_full : scale_last) : 0.f;
       f32x4 dy[2];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1193,7 +1174,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         dh3[t] = s;
       }
       float prox_acc = 0.f;
-      if (last_ch) ++step;
+      ++step;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -1223,7 +1204,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
       HSTAMP(ms, 8);
       // ---- dW1^T (own columns) = X^T dH1
-      constexpr bool PIPE = FEDMX_HW_PIPE && !PROX && !MULTI;
+      constexpr bool PIPE = FEDMX_HW_PIPE && !PROX;
 #pragma unroll
       for (int s = 0; s < KB; ++s) {
         if (SPL) {   // hidden tile 0 only
@@ -1283,31 +1264,26 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         }
       } else {
         // W1 first: the next chunk's layer-1 product waits on it
-        if (last_ch) {
 #pragma unroll
-          for (int t = 0; t < (SPL ? 1 : 2); ++t)
+        for (int t = 0; t < (SPL ? 1 : 2); ++t)
 #pragma unroll
-            for (int v = 0; v < 2; ++v) adam_w1(t, v);
-        }
+          for (int v = 0; v < 2; ++v) adam_w1(t, v);
         HSTAMP(ms, 10);
         // (after an epoch's last batch this works on a stale tile; unused)
         finalize_chunk(nxt);
         l1_partial(nxt, l1a, l1b);
       }
-      if (last_ch) {
-        if (!(FEDMX_HW_ABLATE & 4)) {
-          if (FEDMX_HW_PACKED && !PROX)
-            adam4_packed(P.o, M.o, V.o, Go, K);
-          else
-            adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
-        }
-        if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
-        if (!(FEDMX_HW_ABLATE & 4)) own_to_lds(P, L);   // read by every wave after barrier #1
+      if (!(FEDMX_HW_ABLATE & 4)) {
+        if (FEDMX_HW_PACKED && !PROX)
+          adam4_packed(P.o, M.o, V.o, Go, K);
+        else
+          adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
       }
+      if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
+      if (!(FEDMX_HW_ABLATE & 4)) own_to_lds(P, L);   // read by every wave after barrier #1
       HSTAMP(ms, 11);
       __builtin_amdgcn_iglp_opt(0);
       cur = nxt;
-      }
     }
     w1_to_lds(P, L, SPL ? 1 : 2);   // W1 master (validation, snapshot; SPLIT: rows 16..31 are the helper's)
     double prox_now = 0.0;
@@ -1365,21 +1341,13 @@ extern "C" {
 int fedmx_train_hw(const void* args, int k, hipStream_t stream) {
   if (k <= 0) return 0;
   const fedmx::TrainArgs& A = *reinterpret_cast<const fedmx::TrainArgs*>(args);
-  if (!(A.batch >= 1 && A.d_in >= 1 && A.d_in <= fedmx::DP - 1 && A.hidden >= 1 && A.hidden <= 27 &&
-        A.latent >= 1 && A.latent <= 7))
+  if (!(A.batch >= 1 && A.batch <= 12 && A.d_in >= 1 && A.d_in <= fedmx::DP - 1 && A.hidden >= 1 &&
+        A.hidden <= 27 && A.latent >= 1 && A.latent <= 7))
     return -4;
-  const bool multi = A.batch > 12;   // 12-row chunks per batch
-  if (A.mu != 0.f) {
-    if (multi)
-      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true, true>), dim3(k), dim3(512), 0, stream, A);
-    else
-      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true, false>), dim3(k), dim3(512), 0, stream, A);
-  } else {
-    if (multi)
-      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<false, true>), dim3(k), dim3(512), 0, stream, A);
-    else
-      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<false, false>), dim3(k), dim3(512), 0, stream, A);
-  }
+  if (A.mu != 0.f)
+    hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true>), dim3(k), dim3(512), 0, stream, A);
+  else
+    hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<false>), dim3(k), dim3(512), 0, stream, A);
   return (int)hipGetLastError();
 }
 
