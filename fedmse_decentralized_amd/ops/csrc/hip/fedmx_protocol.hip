@@ -488,7 +488,8 @@ static_assert(sizeof(VerifyArgs) == sizeof(DecideArgs) + 48, "VerifyArgs layout 
 #ifndef FEDMX_VERIFY_ABLATE
 #define FEDMX_VERIFY_ABLATE 0
 #endif
-template <bool CP>
+// REL: the relative drift limit (mode 3) is compiled in only where it is used
+template <bool CP, bool REL>
 __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) {
   const DecideArgs& A = V.D;
   __shared__ __attribute__((aligned(16))) float sW1[HP * S_W1];
@@ -578,7 +579,7 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     // thread's loads are issued before the first add: one memory round trip
     // instead of one per 4 elements (6 dependent rounds, ~5 us of the kernel).
     float drift = 0.f, hnorm = 0.f;
-    const bool rel = A.mode == 3;
+    const bool rel = REL && A.mode == 3;
     if (had_hist && (A.mode == 0 || rel) && !(FEDMX_VERIFY_ABLATE & 2)) {
       const float* h = A.hist + off;
       constexpr int NJ = (P_PAD + 1023) / 1024;
@@ -774,10 +775,17 @@ int fedmx_verify_decide(const void* args, hipStream_t stream) {
   // n_local verification workgroups + n_local snapshot-copy workgroups
   const dim3 grid(V.D.n_local > 0 ? 2 * V.D.n_local : 1);
   // compact forward order for the reference shapes (fedmx_forward_common.h)
-  if (V.D.d_in <= 115 && V.hidden <= 27 && V.latent <= 7)
-    hipLaunchKernelGGL(fedmx::verify_decide_kernel<true>, grid, dim3(512), 0, stream, V);
-  else
-    hipLaunchKernelGGL(fedmx::verify_decide_kernel<false>, grid, dim3(512), 0, stream, V);
+  const bool cp = V.D.d_in <= 115 && V.hidden <= 27 && V.latent <= 7;
+  if (V.D.mode == 3) {
+    if (cp)
+      hipLaunchKernelGGL((fedmx::verify_decide_kernel<true, true>), grid, dim3(512), 0, stream, V);
+    else
+      hipLaunchKernelGGL((fedmx::verify_decide_kernel<false, true>), grid, dim3(512), 0, stream, V);
+  } else if (cp) {
+    hipLaunchKernelGGL((fedmx::verify_decide_kernel<true, false>), grid, dim3(512), 0, stream, V);
+  } else {
+    hipLaunchKernelGGL((fedmx::verify_decide_kernel<false, false>), grid, dim3(512), 0, stream, V);
+  }
   return (int)hipGetLastError();
 }
 
