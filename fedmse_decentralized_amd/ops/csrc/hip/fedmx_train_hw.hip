@@ -79,6 +79,9 @@
 // backward -> Adam -> layer-1 chain instead of the main wave running it
 // alone.  The helpers' W4 Adam moves behind barrier #1 (it overlaps the
 // mains' layers 2-3) and is handed to the mains' layer 4 through an LDS flag.
+#ifndef FEDMX_HW_IGLP
+#define FEDMX_HW_IGLP 0   // the step loop's iglp_opt strategy (-1: none; experiment)
+#endif
 #ifndef FEDMX_HW_RED8
 #define FEDMX_HW_RED8 0   // (experiment) the eight dH3 partial reads after barrier #2 issued together
 #endif
@@ -1282,7 +1285,9 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
       if (!(FEDMX_HW_ABLATE & 4)) own_to_lds(P, L);   // read by every wave after barrier #1
       HSTAMP(ms, 11);
-      __builtin_amdgcn_iglp_opt(0);
+#if FEDMX_HW_IGLP >= 0
+      __builtin_amdgcn_iglp_opt(FEDMX_HW_IGLP);
+#endif
       cur = nxt;
     }
     w1_to_lds(P, L, SPL ? 1 : 2);   // W1 master (validation, snapshot; SPLIT: rows 16..31 are the helper's)

@@ -29,6 +29,8 @@ VARIANTS = {
     "pipe": ["-DFEDMX_HW_PIPE=1"],                   # r4: W1 Adam / next layer-1 software-pipelined by half-tile
     "flags_pipe": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_PIPE=1"],
     "hwsplit": ["-DFEDMX_HW_SPLIT=1"],               # r4: layer-1 hidden tile 1 + its backward / Adam on the helpers
+    "noiglp": ["-DFEDMX_HW_IGLP=-1"],               # r4: no iglp_opt hint in the step loop
+    "iglp1": ["-DFEDMX_HW_IGLP=1"],                 # r4: iglp_opt(1) in the step loop
     "red8": ["-DFEDMX_HW_RED8=1"],                   # r4: dH3 partial reads issued together (the ISA co-simulation predicts -4.6 %)
     "hwsplitd1": ["-DFEDMX_HW_SPLIT=1", "-DFEDMX_HW_SPLIT_DEBUG=1"],   # diagnosis only
     "hwsplitd2": ["-DFEDMX_HW_SPLIT=1", "-DFEDMX_HW_SPLIT_DEBUG=2"],   # diagnosis only
