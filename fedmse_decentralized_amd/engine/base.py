@@ -100,10 +100,11 @@ class ClientStore:
         self.test_label = None
 
     # zero rows after the last client's training rows: the helper-wave
-    # kernel's batch loads (batch <= 12) read whole 12-row chunks without
-    # clamping rows past a client's end (those columns are masked).  Contract
-    # checked by ops/_hip.TrainBuffers before the first launch on a store:
-    # >= 11 rows after the last client, column DP-1 of train/valid holding 1
+    # kernel's batch loads read whole 12-row (batch <= 12) or 16-row (larger
+    # batches) chunks without clamping rows past a client's end (those
+    # columns are masked).  Contract checked by ops/_hip.TrainBuffers before
+    # the first launch on a store: >= 15 rows after the last client, column
+    # DP-1 of train/valid holding 1
     # (``bias_column_rows`` records which buffers _concat filled).
     TRAIN_TAIL_ROWS = 16
 

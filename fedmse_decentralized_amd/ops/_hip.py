@@ -700,11 +700,11 @@ class TrainBuffers:
     def __init__(self, store):
         dev = store.params.device
         # the helper-wave kernel's data contract (engine/base.ClientStore):
-        # whole 12-row chunks are read past the last client's end, and X's
-        # padded column DP-1 is read as the bias input 1
+        # whole 12- or 16-row chunks are read past the last client's end, and
+        # X's padded column DP-1 is read as the bias input 1
         tail = int(store.train.shape[0]) - int(store.train_off[-1])
-        if tail < 11:
-            raise ValueError(f"training buffer needs >= 11 rows after the last client (has {tail}); "
+        if tail < 15:
+            raise ValueError(f"training buffer needs >= 15 rows after the last client (has {tail}); "
                              "build it with ClientStore.load_data")
         if tuple(getattr(store, "bias_column_rows", ())) != ("train", "valid"):
             raise ValueError("training / validation buffers must hold 1 in column DP-1 (ClientStore._concat)")

@@ -1045,8 +1045,12 @@ int fedmx_train(const void* args, int k, hipStream_t stream) {
       A.latent > fedmx::ZP - 1)
     return -3;
   const bool one = A.batch <= 16;
-  const bool cp = A.batch <= 12 && A.hidden <= 27 && A.latent <= 7 && !(A.flags & fedmx::TRAIN_FLAG_NO_COMPACT);
-  const bool hw = cp && !(A.flags & fedmx::TRAIN_FLAG_NO_HELPER) &&
+  // compact layer shapes; the helper-wave kernel takes any batch size there
+  // (batches over 12 rows as 16-row chunks), this kernel's compact order
+  // batches of <= 12 rows
+  const bool cpl = A.hidden <= 27 && A.latent <= 7 && !(A.flags & fedmx::TRAIN_FLAG_NO_COMPACT);
+  const bool cp = A.batch <= 12 && cpl;
+  const bool hw = cpl && !(A.flags & fedmx::TRAIN_FLAG_NO_HELPER) &&
                   (FEDMX_TRAIN_HW_DEFAULT || (A.flags & fedmx::TRAIN_FLAG_HELPER));
   if (hw) return fedmx_train_hw(args, k, stream);
   if (A.mu != 0.f) {

@@ -207,14 +207,24 @@ struct XChunk {
   f32x4 f0, f1, b0, b1;
 };
 
-template <bool PROX>
+// MULTI (batch > 12; VERDICT r3 Next #7, the thesis's batch-64 runs): the
+// step loop runs over 16-row chunks (a batch's chunks in turn, natural batch
+// order, 4 batch k-steps); every chunk is a forward / backward with the
+// step's two barriers, the weight gradients accumulate over the batch's
+// chunks, and Adam plus the W4 / scalar hand-off follow the batch's last
+// chunk.  Loss and gradient scales use the batch's row count, the column
+// masks the chunk's.  (A first version in 12-row compact-order chunks ran
+// 15 % slower than the 4-wave kernel at batch 64: six chunks per batch
+// instead of four.)
+template <bool PROX, bool MULTI>
 __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // the flag hand-offs measured faster with FedProx only (profiles/r4_train_hw_experiments.md)
-  constexpr int HWF = PROX ? FEDMX_HW_FLAGS_PROX : FEDMX_HW_FLAGS;
-  constexpr bool SPL = FEDMX_HW_SPLIT && !PROX && !HWF;
+  constexpr int HWF = MULTI ? 0 : (PROX ? FEDMX_HW_FLAGS_PROX : FEDMX_HW_FLAGS);
+  constexpr bool SPL = FEDMX_HW_SPLIT && !PROX && !HWF && !MULTI;
   constexpr bool W4FLAG = HWF || SPL;   // W4 / Adam scalars handed over by LDS flag (per-helper K slots)
   constexpr bool CP = true;
-  constexpr int KB = 3;   // k-steps of products over the batch (compact order)
+  constexpr bool CPB = !MULTI;       // compact batch order (12 rows of 16 columns)
+  constexpr int KB = CPB ? 3 : 4;    // k-steps of products over the batch
   constexpr int KZ = 2;   // k-steps of products over the latent axis
   __shared__ __attribute__((aligned(16))) float lds[L_TOTAL];
   const int w8 = threadIdx.x >> 6;
@@ -306,6 +316,8 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   const float* const Xva = A.valid_x + (size_t)A.valid_off[cid] * DP;
   const int n_va = (int)(A.valid_off[cid + 1] - A.valid_off[cid]);
   const int nb = (n_tr + B - 1) / B;
+  // MULTI: 16-row chunks per epoch ((nb - 1) full batches + the last one)
+  const int nsteps = MULTI ? (nb > 0 ? (nb - 1) * ((B + 15) / 16) + (n_tr - (nb - 1) * B + 15) / 16 : 0) : nb;
   const int nvb = (n_va + B - 1) / B;
   const int nvt = (n_va + 15) / 16;   // 16-row validation tiles
   int step = A.adam_step[cid];
@@ -332,10 +344,10 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     zreal_d[r] = j < latent;
     zbias_d[r] = j == z_bias_slot<CP>();
   }
-  const int brow_c = batch_row_of_col<CP>(c);
+  const int brow_c = batch_row_of_col<CPB>(c);
   int brow_b[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) brow_b[r] = batch_row_of_col<CP>(4 * g + r);
+  for (int r = 0; r < 4; ++r) brow_b[r] = batch_row_of_col<CPB>(4 * g + r);
 
   // one batch chunk of X in both register layouts the step uses (f: layer
   // 1's B operand over this wave's 32 columns; b: dW1's, batch on k);
@@ -346,21 +358,23 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // row base plus a per-lane offset formed once, with no per-step clamping.
   // (padding columns, brow_c = -1, read the chunk's row 0; every row < 12)
   const unsigned offf = (unsigned)((brow_c < 0 ? 0 : brow_c) * DP + xcol);
-  unsigned offb[3];
+  unsigned offb[KB];
 #pragma unroll
-  for (int r = 0; r < 3; ++r) offb[r] = (unsigned)(brow_b[r] * DP + 32 * w + c);   // r < 3: real rows
+  for (int r = 0; r < KB; ++r) offb[r] = (unsigned)(brow_b[r] * DP + 32 * w + c);   // CPB: r < 3 real rows
   auto load_chunk = [&](const float* X, int row0, int bc, XChunk& x) {
     (void)bc;
     const float* base = X + (size_t)row0 * DP;
     x.f0 = *reinterpret_cast<const f32x4*>(base + offf);
     x.f1 = *reinterpret_cast<const f32x4*>(base + offf + 16);   // cols DP-4..DP-1 on the bias lane
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {   // row quad 3 is padding, never read
+    for (int r = 0; r < KB; ++r) {   // CPB: row quad 3 is padding, never read
       x.b0[r] = base[offb[r]];
       x.b1[r] = base[offb[r] + 16];
     }
-    x.b0[3] = 0.f;
-    x.b1[3] = 0.f;
+    if (CPB) {
+      x.b0[3] = 0.f;
+      x.b1[3] = 0.f;
+    }
   };
   // (FEDMX_HW_XBIAS: the packed rows already hold the 1 in column DP-1,
   // ClientStore._concat -- nothing to overwrite after the load)
@@ -826,8 +840,21 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     for (int ep = 0; ep < A.epochs; ++ep) {
       double acc_tr = 0.0;
       // W4 gradient + Adam between barrier #2 of step s and barrier #1 of s+1
-      for (int bi = 0; bi < nb; ++bi) {
+      int mb = 0, mch = 0;   // MULTI: batch / chunk of this step
+      f32x4 G4[2][2];
+      for (int bi = 0; bi < nsteps; ++bi) {
         const bool hs = (ep == 0 && bi == STAMP_STEP);
+        const int nch = MULTI ? (min(B, n_tr - mb * B) + 15) / 16 : 1;
+        const bool first_ch = !MULTI || mch == 0;
+        const bool last_ch = !MULTI || mch + 1 == nch;
+        if (MULTI) {
+          if (last_ch) {
+            ++mb;
+            mch = 0;
+          } else {
+            ++mch;
+          }
+        }
         HSTAMP(hs, 0);
         if (!HWF) __syncthreads();   // barrier #1 (main: layer-1 partials)
         HSTAMP(hs, 2);
@@ -846,11 +873,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         const f32x4 w4a1 = lds_read4(sT0 + tr + 16 * S_T);
         const f32x4 w4b0 = lds_read4(sT1 + tr);
         const f32x4 w4b1 = lds_read4(sT1 + tr + 16 * S_T);
-        f32x4 G4[2][2];
+        if (first_ch) {
 #pragma unroll
-        for (int v = 0; v < 2; ++v)
+          for (int v = 0; v < 2; ++v)
 #pragma unroll
-          for (int t = 0; t < 2; ++t) G4[v][t] = zero4();
+            for (int t = 0; t < 2; ++t) G4[v][t] = zero4();
+        }
 #pragma unroll
         for (int s = 0; s < KB; ++s) {
           G4[0][0] = mfma16(w4a0[s], w4b0[s], G4[0][0]);
@@ -858,6 +886,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           G4[1][0] = mfma16(w4a1[s], w4b0[s], G4[1][0]);
           G4[1][1] = mfma16(w4a1[s], w4b1[s], G4[1][1]);
         }
+        if (!last_ch) continue;   // MULTI: W4's Adam after the batch's last chunk
         HSTAMP(hs, 8);
         float prox_acc = 0.f;
 #pragma unroll
@@ -970,20 +999,39 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       finalize_chunk(cur);
       l1_partial(cur, l1a, l1b);
     }
-    for (int bi = 0; bi < nb; ++bi) {
-      const int row_b = bi * B;
-      const int bt = min(B, n_tr - row_b);
-      const bool has_next = bi + 1 < nb;
-      const int row_n = (bi + 1) * B;
+    int mb = 0, mch = 0;   // MULTI: batch / chunk of this step
+    f32x4 G1[2][2], Go;
+    for (int bi = 0; bi < nsteps; ++bi) {
+      // MULTI: this step is chunk mch of batch mb (16 rows from row_b); the
+      // batch's row count bt sets the scales, the chunk's bc the masks
+      const int row_b = MULTI ? mb * B + 16 * mch : bi * B;
+      const int bt = MULTI ? min(B, n_tr - mb * B) : min(B, n_tr - row_b);
+      const int nch = MULTI ? (bt + 15) / 16 : 1;
+      const bool first_ch = !MULTI || mch == 0;
+      const bool last_ch = !MULTI || mch + 1 == nch;
+      const int bc = MULTI ? min(16, bt - 16 * mch) : bt;
+      const bool has_next_b = MULTI ? mb + 1 < nb : bi + 1 < nb;
+      const bool has_next = MULTI ? (!last_ch || has_next_b) : has_next_b;
+      const int row_n = MULTI ? (last_ch ? (mb + 1) * B : row_b + 16) : (bi + 1) * B;
       const int bc_n = has_next ? min(B, n_tr - row_n) : 0;
-      const float inv_bt = has_next ? inv_b_full : inv_b_last;
+      const float inv_bt = has_next_b ? inv_b_full : inv_b_last;
+      if (MULTI) {
+        if (last_ch) {
+          ++mb;
+          mch = 0;
+        } else {
+          ++mch;
+        }
+      }
       const bool ms = (ep == 0 && bi == STAMP_STEP);
       HSTAMP(ms, 0);
-      f32x4 G1[2][2], Go = zero4();
+      if (first_ch) {
+        Go = zero4();
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int v = 0; v < 2; ++v) G1[t][v] = zero4();
+          for (int v = 0; v < 2; ++v) G1[t][v] = zero4();
+      }
 
       // ---- forward: layer-1 K reduction (barrier #1), layers 2-4, loss
       f32x4 h1[2], z, zb, h3[2], y[2], q4[2][2];
@@ -1065,7 +1113,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           flag_wait(4 + w, 1, js + 1);   // helper w has published W4(s) and the scalars
           read_helper_state();
         }
-        ++js;
+        if (last_ch) ++js;
         {
           f32x4 acc0 = zero4(), acc1 = zero4();
           const f32x4 a00 = lds_read4(a4p);
@@ -1092,7 +1140,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           const float d1 = (bias_lane && r == 3) ? 0.f : y[1][r] - cur.f1[r];
           sq += d0 * d0 + d1 * d1;
         }
-        const bool col_ok = (unsigned)brow_c < (unsigned)bt;
+        const bool col_ok = (unsigned)brow_c < (unsigned)bc;
         sq = col_ok ? sq : 0.f;
         float nz = 0.f;
 #pragma unroll
@@ -1116,8 +1164,8 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         }
 
       // ---- dY (masked, feature-major); dY^T / H3^T for the helper's dW4
-      const bool col_ok = (unsigned)brow_c < (unsigned)bt;
-      const float scale = col_ok ? (has_next ? scale_full : scale_last) : 0.f;
+      const bool col_ok = (unsigned)brow_c < (unsigned)bc;
+      const float scale = col_ok ? (has_next_b ? scale_full : scale_last) : 0.f;
       f32x4 dy[2];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1177,7 +1225,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         dh3[t] = s;
       }
       float prox_acc = 0.f;
-      ++step;
+      if (last_ch) ++step;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -1207,7 +1255,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
       HSTAMP(ms, 8);
       // ---- dW1^T (own columns) = X^T dH1
-      constexpr bool PIPE = FEDMX_HW_PIPE && !PROX;
+      constexpr bool PIPE = FEDMX_HW_PIPE && !PROX && !MULTI;
 #pragma unroll
       for (int s = 0; s < KB; ++s) {
         if (SPL) {   // hidden tile 0 only
@@ -1267,23 +1315,28 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         }
       } else {
         // W1 first: the next chunk's layer-1 product waits on it
+        // (MULTI: the batch's last chunk only)
+        if (last_ch) {
 #pragma unroll
-        for (int t = 0; t < (SPL ? 1 : 2); ++t)
+          for (int t = 0; t < (SPL ? 1 : 2); ++t)
 #pragma unroll
-          for (int v = 0; v < 2; ++v) adam_w1(t, v);
+            for (int v = 0; v < 2; ++v) adam_w1(t, v);
+        }
         HSTAMP(ms, 10);
         // (after an epoch's last batch this works on a stale tile; unused)
         finalize_chunk(nxt);
         l1_partial(nxt, l1a, l1b);
       }
-      if (!(FEDMX_HW_ABLATE & 4)) {
-        if (FEDMX_HW_PACKED && !PROX)
-          adam4_packed(P.o, M.o, V.o, Go, K);
-        else
-          adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
+      if (last_ch) {
+        if (!(FEDMX_HW_ABLATE & 4)) {
+          if (FEDMX_HW_PACKED && !PROX)
+            adam4_packed(P.o, M.o, V.o, Go, K);
+          else
+            adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
+        }
+        if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
+        if (!(FEDMX_HW_ABLATE & 4)) own_to_lds(P, L);   // read by every wave after barrier #1
       }
-      if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
-      if (!(FEDMX_HW_ABLATE & 4)) own_to_lds(P, L);   // read by every wave after barrier #1
       HSTAMP(ms, 11);
 #if FEDMX_HW_IGLP >= 0
       __builtin_amdgcn_iglp_opt(FEDMX_HW_IGLP);
@@ -1346,13 +1399,21 @@ extern "C" {
 int fedmx_train_hw(const void* args, int k, hipStream_t stream) {
   if (k <= 0) return 0;
   const fedmx::TrainArgs& A = *reinterpret_cast<const fedmx::TrainArgs*>(args);
-  if (!(A.batch >= 1 && A.batch <= 12 && A.d_in >= 1 && A.d_in <= fedmx::DP - 1 && A.hidden >= 1 &&
-        A.hidden <= 27 && A.latent >= 1 && A.latent <= 7))
+  if (!(A.batch >= 1 && A.d_in >= 1 && A.d_in <= fedmx::DP - 1 && A.hidden >= 1 && A.hidden <= 27 &&
+        A.latent >= 1 && A.latent <= 7))
     return -4;
-  if (A.mu != 0.f)
-    hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true>), dim3(k), dim3(512), 0, stream, A);
-  else
-    hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<false>), dim3(k), dim3(512), 0, stream, A);
+  const bool multi = A.batch > 12;   // 16-row chunks per batch
+  if (A.mu != 0.f) {
+    if (multi)
+      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true, true>), dim3(k), dim3(512), 0, stream, A);
+    else
+      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true, false>), dim3(k), dim3(512), 0, stream, A);
+  } else {
+    if (multi)
+      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<false, true>), dim3(k), dim3(512), 0, stream, A);
+    else
+      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<false, false>), dim3(k), dim3(512), 0, stream, A);
+  }
   return (int)hipGetLastError();
 }
 

@@ -81,6 +81,12 @@ def main():
     _hip.TRAIN_COMPACT = False   # identity internal order (no padded k-steps skipped)
     out["train_launch_identity_order_us"] = timeit(lambda: eng.train_async(sel, hp), reps=args.reps)[0]
     _hip.TRAIN_COMPACT = True
+    # batch 64 (the thesis's GPU runs): helper-wave kernel (16-row chunks) vs the 4-wave kernel
+    hp64 = TrainHParams(epochs=args.epochs, batch_size=64, lr=1e-3, shrink_lambda=5.0, patience=10 ** 6)
+    out["train_launch_b64_us"] = timeit(lambda: eng.train_async(sel, hp64), reps=args.reps)[0]
+    prev, _hip.TRAIN_HELPER = _hip.TRAIN_HELPER, False
+    out["train_launch_b64_4wave_us"] = timeit(lambda: eng.train_async(sel, hp64), reps=args.reps)[0]
+    _hip.TRAIN_HELPER = prev
     if args.train_only:
         print(json.dumps({k: round(v, 3) if isinstance(v, float) else v for k, v in out.items()}))
         return

@@ -223,6 +223,33 @@ def test_train_kernel_helper_waves_match_four_waves(batch, lam, mu, epochs, pati
             assert torch.equal(getattr(a.store, name), getattr(b.store, name)), name
 
 
+@pytest.mark.parametrize("batch,lam,mu", [(64, 5.0, 0.0), (33, 1.0, 0.001), (13, 5.0, 0.0), (128, 0.0, 0.01)])
+def test_train_kernel_helper_waves_multi_chunk_batches(batch, lam, mu):
+    """Batches over 12 rows on the helper-wave kernel (16-row chunks, weight
+    gradients accumulated over a batch's chunks, one Adam step per batch)
+    against the 4-wave kernel (also 16-row chunks): the same training up to
+    the fp32 summation order of the two kernels' products (VERDICT r3 Next
+    #7; the kernel-vs-oracle test covers batch 16 / 33 / 64 / 128 too)."""
+    _, a = _setup_pair(n_train=(301, 150), n_valid=(70, 33), seed=17)
+    _, b = _setup_pair(n_train=(301, 150), n_valid=(70, 33), seed=17)
+    anchor = a.store.params + 0.01 * torch.randn(a.store.params.shape, generator=torch.Generator().manual_seed(8),
+                                                 device="cpu").to(DEV)
+    anchor = canonical_to_padded(padded_to_canonical(anchor.cpu())).to(DEV)
+    a.store.anchor.copy_(anchor)
+    b.store.anchor.copy_(anchor)
+    hp = TrainHParams(epochs=3, batch_size=batch, lr=1e-3, shrink_lambda=lam, fedprox_mu=mu, patience=10 ** 6)
+    for _ in range(2):   # second launch: persistent Adam state and step counts
+        ta, ea, ba = _hip.train(a.store, [0, 1], hp, a.dims, helper=True)
+        tb, eb, bb = _hip.train(b.store, [0, 1], hp, b.dims, helper=False)
+        torch.cuda.synchronize()
+        _hip.runtime(DEV).sync()
+        assert list(ea) == list(eb) and list(ba) == list(bb)
+        np.testing.assert_allclose(np.array(ta), np.array(tb), rtol=1e-5, atol=1e-7)
+        for name in ("params", "best", "adam_m", "adam_v"):
+            torch.testing.assert_close(getattr(a.store, name), getattr(b.store, name), rtol=1e-3, atol=1e-6)
+        assert torch.equal(a.store.adam_step, b.store.adam_step)
+
+
 def test_train_kernel_single_step_tight():
     # one Adam step from identical state: errors are pure fp32 rounding
     ref, hip = _setup_pair(n_train=(12,), n_valid=(12,), seed=3)
