@@ -14,11 +14,11 @@ from fedmse_decentralized_amd.config import ExperimentConfig
 from test_device_protocol_gpu import _shrink
 
 
-def _run(out, backend, device, model_type, update_type, rounds=3):
+def _run(out, backend, device, model_type, update_type, rounds=3, batch_size=12):
     from fedmse_decentralized_amd import federation
     from fedmse_decentralized_amd.federation import Federation
 
-    cfg = ExperimentConfig(synthetic="nbaiot", network_size=6, num_rounds=rounds, epoch=2, batch_size=12,
+    cfg = ExperimentConfig(synthetic="nbaiot", network_size=6, num_rounds=rounds, epoch=2, batch_size=batch_size,
                            output_root=out, backend=backend, device=device, log_level="WARNING",
                            compat="reference", global_early_stop=False, save_checkpoints=False,
                            model_types=[model_type], update_types=[update_type])
@@ -40,6 +40,22 @@ def test_hip_engine_matches_torch_engine(tmp_path, model_type, update_type):
     fh, rh = _run(str(tmp_path / "hip"), "hip", "cuda", model_type, update_type)
     ft, rt = _run(str(tmp_path / "torch"), "torch", "cpu", model_type, update_type)
     assert fh.engine.name == "hip" and ft.engine.name == "torch"
+    for a, b in zip(rh, rt):
+        assert a.selected == b.selected
+        assert a.aggregator == b.aggregator
+        assert a.verification == b.verification
+        np.testing.assert_allclose(np.array(a.metrics), np.array(b.metrics), atol=2e-3)
+    torch.testing.assert_close(fh.engine.store.params.cpu(), ft.engine.store.params, rtol=2e-2, atol=2e-4)
+
+
+@pytest.mark.parametrize("update_type", ["mse_avg", "fedprox"])
+def test_hip_engine_matches_torch_engine_batch_64(tmp_path, update_type):
+    """The thesis's batch-64 configuration end to end: the helper-wave
+    kernel's 16-row-chunk path (batches over 12 rows) inside the federation,
+    against the CPU oracle."""
+    _shrink()
+    fh, rh = _run(str(tmp_path / "hip"), "hip", "cuda", "hybrid", update_type, batch_size=64)
+    ft, rt = _run(str(tmp_path / "torch"), "torch", "cpu", "hybrid", update_type, batch_size=64)
     for a, b in zip(rh, rt):
         assert a.selected == b.selected
         assert a.aggregator == b.aggregator
