@@ -79,6 +79,9 @@
 // backward -> Adam -> layer-1 chain instead of the main wave running it
 // alone.  The helpers' W4 Adam moves behind barrier #1 (it overlaps the
 // mains' layers 2-3) and is handed to the mains' layer 4 through an LDS flag.
+#ifndef FEDMX_HW_SIMK
+#define FEDMX_HW_SIMK 0
+#endif
 #ifndef FEDMX_HW_IGLP
 #define FEDMX_HW_IGLP 0   // the step loop's iglp_opt strategy (-1: none; experiment)
 #endif
@@ -521,6 +524,13 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   double b1pow = pow((double)A.beta1, (double)step);
   double b2pow = pow((double)A.beta2, (double)step);
   auto next_constants = [&]() {
+#if FEDMX_HW_SIMK   // (co-simulation probe only: wrong numerics) scalars from LDS instead of f64 math
+    const f32x4 kk = lds_read4(sK + 16);
+    K.neg_step_size = kk[0];
+    K.bc2s = kk[1];
+    K.inv_bc2s = kk[2];
+    return;
+#endif
     b1pow *= (double)A.beta1;
     b2pow *= (double)A.beta2;
     K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));

@@ -68,10 +68,13 @@ def split_operands(ops: str):
     return parts
 
 
+MFMA_VPORT_HOLD = 8   # cycles an MFMA holds the SIMD's vector issue (--mfma-hold)
+
+
 def classify(op: str):
     """(kind, issue cycles, result latency)."""
     if op in MFMA_PIPE:
-        return "mfma", 8, MFMA_PIPE[op][1]
+        return "mfma", MFMA_VPORT_HOLD, MFMA_PIPE[op][1]
     if op.startswith("ds_read") or op.startswith("ds_bpermute") or op.startswith("ds_swizzle") \
             or op.startswith("ds_permute") or op.startswith("ds_load"):
         return "lds_read", 4, LDS_LAT + (LDS_B128 if "b128" in op else 0)
@@ -211,14 +214,17 @@ def lds_bytes(op: str) -> int:
     return 64 * width
 
 
-def cosim(bodies, names, iters=6, max_cycles=2_000_000, lds_bw=0.0):
+def cosim(bodies, names, iters=6, max_cycles=2_000_000, lds_bw=0.0, lds_queue=None):
     """Cycle-stepped co-simulation of the waves sharing ONE SIMD (the main
     wave and its helper): one matrix pipe, one vector issue port (VALU issue
     4 cycles, an MFMA holds it 8), per-wave in-order issue, priority by age
     (the first body first), and the loop's workgroup barriers joined by both
     (the waves on the other SIMDs are taken to arrive with them).  lds_bw > 0:
     this SIMD's share of the CU's LDS bandwidth in bytes per cycle (the other
-    three SIMDs taken to run the same stream), shared by both waves."""
+    three SIMDs taken to run the same stream), shared by both waves.
+    lds_queue (cycles, with lds_bw): an LDS instruction cannot issue while
+    the SIMD's LDS backlog exceeds it -- the wave stalls at issue, and so
+    does everything behind it in program order (SQ_WAIT_INST_LDS)."""
     ws = [_Wave(b, n) for b, n in zip(bodies, names)]
     mfma_free = vport_free = lds_free = 0
     t = 0
@@ -237,6 +243,8 @@ def cosim(bodies, names, iters=6, max_cycles=2_000_000, lds_bw=0.0):
                 why = "vector port (other wave)"
             if why is None and kind == "mfma" and mfma_free > t:
                 why = "matrix pipe busy"
+            if why is None and lds_queue is not None and kind in ("lds_read", "lds_write") and lds_free - t > lds_queue:
+                why = "LDS issue (queue full)"
             if why is None and kind == "wait":
                 for cnt, q in (("lgkmcnt", w.lds_q), ("vmcnt", w.vm_q)):
                     m = re.search(cnt + r"\((\d+)\)", raw)
@@ -321,9 +329,16 @@ def main(argv=None) -> int:
     p.add_argument("--top", type=int, default=25)
     p.add_argument("--lds-bw", type=float, default=0.0,
                    help="co-simulation: this SIMD's LDS bandwidth share, bytes/cycle (0: unlimited)")
+    p.add_argument("--lds-queue", type=float, default=None,
+                   help="co-simulation with --lds-bw: LDS backlog (cycles) above which an LDS instruction stalls at issue")
+    p.add_argument("--mfma-hold", type=int, default=None,
+                   help="cycles an MFMA holds the vector issue port (default 8; 32 = no VALU co-execution)")
     p.add_argument("--cosim", action="store_true",
                    help="also co-simulate the main loop with the helper loop (the 2-barrier loop with fewest MFMAs)")
     a = p.parse_args(argv)
+    if a.mfma_hold is not None:
+        global MFMA_VPORT_HOLD
+        MFMA_VPORT_HOLD = a.mfma_hold
     lines = open(a.asm).read().split("\n")
     files = {}
     for l in lines:
@@ -397,7 +412,7 @@ def main(argv=None) -> int:
         def rot(b):
             i = next(k for k, x in enumerate(b) if x[0] == "s_barrier")
             return b[i:] + b[:i]
-        ws = cosim([rot(body), rot(hbody)], ["main", "helper"], lds_bw=a.lds_bw)
+        ws = cosim([rot(body), rot(hbody)], ["main", "helper"], lds_bw=a.lds_bw, lds_queue=a.lds_queue)
         print(f"co-simulation on one SIMD: main loop {lp['label']} + helper loop {hl['label']} "
               f"({hl['mfma']} MFMA)")
         for w in ws:
