@@ -63,40 +63,14 @@
 #ifndef FEDMX_HW_FLAGS_PROX
 #define FEDMX_HW_FLAGS_PROX 1
 #endif
-// 1 (without FedProx): W1's Adam and the next layer-1 product software-
-// pipelined per half of the register tile: Adam of the v = 0 quads, their
-// layer-1 MFMAs, whose issue the v = 1 quads' Adam VALU then fills
-// (same per-accumulator order: bit-identical)
-#ifndef FEDMX_HW_PIPE
-#define FEDMX_HW_PIPE 0
-#endif
-// 1 (without FedProx): SPLIT step.  Layer 1's second hidden tile (W1 rows
-// 16..31 of every main wave's input-feature slice) moves to the helper
-// waves: helper w keeps those W1 entries with their Adam state, recomputes
-// the step's dH3 reduction / dZ (bit-identical, from the same LDS data) to
-// form its half of dH1, its half of dW1, their Adam update and its half of
-// the next layer-1 partial.  Each SIMD's two waves then share the serial
-// backward -> Adam -> layer-1 chain instead of the main wave running it
-// alone.  The helpers' W4 Adam moves behind barrier #1 (it overlaps the
-// mains' layers 2-3) and is handed to the mains' layer 4 through an LDS flag.
-#ifndef FEDMX_HW_SIMK
-#define FEDMX_HW_SIMK 0
-#endif
+// (Round 4 also measured, and removed, four more variants of this step: a
+// software-pipelined W1 Adam / layer-1 (+4.2 %), the SPLIT step with layer 1's
+// second hidden tile and its backward on the helpers (+22.6 %), the eight dH3
+// partial reads issued together (+6.5 %, LDS issue stalls) and a co-simulation
+// probe; profiles/r4_train_hw_experiments.md, source in git history before
+// this note.)
 #ifndef FEDMX_HW_IGLP
-#define FEDMX_HW_IGLP 0   // the step loop's iglp_opt strategy (-1: none; experiment)
-#endif
-#ifndef FEDMX_HW_RED8
-#define FEDMX_HW_RED8 0   // (experiment) the eight dH3 partial reads after barrier #2 issued together
-#endif
-#ifndef FEDMX_HW_SPLIT
-#define FEDMX_HW_SPLIT 0
-#endif
-// debug bits for SPLIT (diagnosis builds only): 1 = the mains also form
-// layer 1's hidden tile 1 and write it instead of the helpers; 2 = the mains
-// also form it, and both roles dump their tile-1 partial of the launch's first
-// step (workgroup 0) into A.stamps (mains [0, 1024), helpers [1024, 2048))
-#ifndef FEDMX_HW_SPLIT_DEBUG
-#define FEDMX_HW_SPLIT_DEBUG 0
+#define FEDMX_HW_IGLP 0   // the step loop's iglp_opt strategy (-1: none; r4 A/B: +12.6 %, 1: +1.6 %)
 #endif
 // bound on one flag wait (polls); a wait that runs out marks the launch failed
 // (epochs_run = -1000) instead of hanging the GPU
@@ -156,9 +130,9 @@ struct Lane {
   int own_stride;
 };
 
-__device__ __forceinline__ void w1_to_lds(const MSlab& o, const Lane& L, int t_end = 2) {
+__device__ __forceinline__ void w1_to_lds(const MSlab& o, const Lane& L) {
 #pragma unroll
-  for (int t = 0; t < t_end; ++t)
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int v = 0; v < 2; ++v)
       lds_write4(L.w1 + 16 * t * S_W1 + 16 * v, f32x4{o.q1[t][v][0], o.q1[t][v][1], o.q1[t][v][2], o.q1[t][v][3]});
@@ -223,8 +197,7 @@ template <bool PROX, bool MULTI>
 __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // the flag hand-offs measured faster with FedProx only (profiles/r4_train_hw_experiments.md)
   constexpr int HWF = MULTI ? 0 : (PROX ? FEDMX_HW_FLAGS_PROX : FEDMX_HW_FLAGS);
-  constexpr bool SPL = FEDMX_HW_SPLIT && !PROX && !HWF && !MULTI;
-  constexpr bool W4FLAG = HWF || SPL;   // W4 / Adam scalars handed over by LDS flag (per-helper K slots)
+  constexpr bool W4FLAG = HWF != 0;   // W4 / Adam scalars handed over by LDS flag (per-helper K slots)
   constexpr bool CP = true;
   constexpr bool CPB = !MULTI;       // compact batch order (12 rows of 16 columns)
   constexpr int KB = CPB ? 3 : 4;    // k-steps of products over the batch
@@ -524,13 +497,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   double b1pow = pow((double)A.beta1, (double)step);
   double b2pow = pow((double)A.beta2, (double)step);
   auto next_constants = [&]() {
-#if FEDMX_HW_SIMK   // (co-simulation probe only: wrong numerics) scalars from LDS instead of f64 math
-    const f32x4 kk = lds_read4(sK + 16);
-    K.neg_step_size = kk[0];
-    K.bc2s = kk[1];
-    K.inv_bc2s = kk[2];
-    return;
-#endif
     b1pow *= (double)A.beta1;
     b2pow *= (double)A.beta2;
     K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
@@ -610,204 +576,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     if (stager) vals_to_masters_o<CP>(v, sW1, sW4, sW2, sW3);
     __syncthreads();
   };
-
-  if (SPL && helper) {
-    // ====================== helper waves, SPLIT step ===============================
-    HSlab P4, M4, V4;
-    float P1[2][4], M1[2][4], V1[2][4];   // W1 rows 16..31 x this wave's 32 input features
-    auto lds_to_w1h = [&](float (&o)[2][4]) {
-#pragma unroll
-      for (int v = 0; v < 2; ++v) {
-        const f32x4 q = lds_read4(L.w1 + 16 * S_W1 + 16 * v);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[v][r] = q[r];
-      }
-    };
-    auto w1h_to_lds = [&](const float (&o)[2][4]) {
-#pragma unroll
-      for (int v = 0; v < 2; ++v) lds_write4(L.w1 + 16 * S_W1 + 16 * v, f32x4{o[v][0], o[v][1], o[v][2], o[v][3]});
-    };
-    stage_vals(pv_m);
-    lds_to_hslab(M4, L);
-    lds_to_w1h(M1);
-    __syncthreads();
-    stage_vals(pv_v);
-    lds_to_hslab(V4, L);
-    lds_to_w1h(V1);
-    __syncthreads();
-    stage_vals(pv_p);
-    lds_to_hslab(P4, L);
-    lds_to_w1h(P1);
-    auto publish_q4 = [&]() {
-#pragma unroll
-      for (int v = 0; v < 2; ++v)
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          lds_write4(q4p + (2 * v + t) * 256, f32x4{P4.q4[v][t][0], P4.q4[v][t][1], P4.q4[v][t][2], P4.q4[v][t][3]});
-    };
-    int js = 0;
-    auto publish_k = [&]() {
-      next_constants();
-      if (lane == 0) lds_write4(sK + 8 * w + 4 * (js & 1), f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f});
-    };
-    publish_q4();
-    publish_k();               // step 0's scalars
-    flag_set(4 + w, 1);        // W4 / scalars of launch step 0 published
-    f32x4 G4[2][2];
-    bool g4_pending = false;
-    // W4's Adam for the gradient of the previous step, then W4(s) published
-    auto apply_w4 = [&]() {
-      float dummy = 0.f;
-      HSlab AN4;
-#pragma unroll
-      for (int v = 0; v < 2; ++v)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) adam4<false>(P4.q4[v][t], M4.q4[v][t], V4.q4[v][t], AN4.q4[v][t], G4[v][t], K,
-                                                 dummy);
-      w4_to_lds(P4, L);
-      publish_q4();
-      ++js;
-      publish_k();
-      flag_set(4 + w, js + 1);
-      g4_pending = false;
-    };
-    auto l1h_partial = [&](const XChunk& x) {
-      f32x4 acc = zero4();
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc = mfma16(P1[0][j], x.f0[j], acc);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc = mfma16(P1[1][j], x.f1[j], acc);
-      return acc;
-    };
-    const int bt_last_h = nb > 0 ? n_tr - (nb - 1) * B : B;
-    for (int ep = 0; ep < A.epochs; ++ep) {
-      XChunk hc, hn;
-      f32x4 l1h = zero4();
-      if (nb > 0) {
-        load_chunk(Xtr, 0, min(B, n_tr), hc);
-        l1h = l1h_partial(hc);
-      }
-      for (int bi = 0; bi < nb; ++bi) {
-        const bool has_next = bi + 1 < nb;
-        const int bt = has_next ? B : bt_last_h;
-        float* red = sRedH1 + parity * L_RED;
-        if ((FEDMX_HW_SPLIT_DEBUG & 2) && ep == 0 && bi == 0 && blockIdx.x == 0 && A.stamps != nullptr) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) A.stamps[1024 + (w * 64 + lane) * 4 + r] = (uint64_t)__float_as_uint(l1h[r]);
-        }
-        if (!(FEDMX_HW_SPLIT_DEBUG & 1))
-          lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1h);   // this wave's half of the layer-1 partial
-        __syncthreads();   // barrier #1
-        parity ^= 1;
-        // W3 / W2 columns of this step: read now, while the masters hold W(s)
-        // (mains 0-3 publish W(s+1) at the end of their segment B, before this
-        // wave's dZ / dH1 below)
-        float q3h[2][4], q2h[4];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) q3h[t][r] = d3p[(16 * t + r) * S_W3];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) q2h[r] = d2p[r * S_W2 + 16];
-        if (g4_pending) apply_w4();
-        __syncthreads();   // barrier #2 (main: dY^T / H3^T / dH3 partials / H1^T / Z^T written)
-        // ---- dW4 (own rows) of this step
-        {
-          const f32x4 w4a0 = lds_read4(sT0 + tr);
-          const f32x4 w4a1 = lds_read4(sT0 + tr + 16 * S_T);
-          const f32x4 w4b0 = lds_read4(sT1 + tr);
-          const f32x4 w4b1 = lds_read4(sT1 + tr + 16 * S_T);
-#pragma unroll
-          for (int v = 0; v < 2; ++v)
-#pragma unroll
-            for (int t = 0; t < 2; ++t) G4[v][t] = zero4();
-#pragma unroll
-          for (int s2 = 0; s2 < KB; ++s2) {
-            G4[0][0] = mfma16(w4a0[s2], w4b0[s2], G4[0][0]);
-            G4[0][1] = mfma16(w4a0[s2], w4b1[s2], G4[0][1]);
-            G4[1][0] = mfma16(w4a1[s2], w4b0[s2], G4[1][0]);
-            G4[1][1] = mfma16(w4a1[s2], w4b1[s2], G4[1][1]);
-          }
-          g4_pending = true;
-        }
-        if (has_next) load_chunk(Xtr, (bi + 1) * B, 0, hn);   // prefetch
-        // ---- dH3 (the mains' reduction, same operands and order) -> dZ
-        f32x4 dh3[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          f32x4 sm = lds_read4(sRedDH3 + t * 256 + lane * 4);
-#pragma unroll
-          for (int ww = 1; ww < 4; ++ww) {
-            const f32x4 o = lds_read4(sRedDH3 + (ww * 2 + t) * 256 + lane * 4);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sm[r] = sm[r] + o[r];
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float h3v = sT1[tw + (16 * t + r) * S_T];   // main w's H3, D layout
-            sm[r] = (hreal_d[t][r] && h3v > 0.f) ? sm[r] : 0.f;
-          }
-          dh3[t] = sm;
-        }
-        float zh[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) zh[r] = sZT[tw + r * S_T];
-        float nz = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) nz += zreal_d[r] ? zh[r] * zh[r] : 0.f;
-        nz = sum_lane_groups(nz);
-        const float norm_h = __builtin_amdgcn_sqrtf(nz);
-        f32x4 dz = chain2(f32x4{q3h[0][0], q3h[0][1], q3h[0][2], q3h[0][3]},
-                          f32x4{q3h[1][0], q3h[1][1], q3h[1][2], q3h[1][3]}, dh3[0], dh3[1]);
-        const bool col_ok = (unsigned)brow_c < (unsigned)bt;
-        const float shr_raw = lam * __builtin_amdgcn_rcpf((float)bt * norm_h);
-        const float shr = (col_ok && norm_h > 0.f) ? shr_raw : 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dz[r] = zreal_d[r] ? dz[r] + shr * zh[r] : 0.f;
-        // ---- dH1 (hidden tile 1, batch-major) -> dW1 rows 16..31 -> Adam
-        f32x4 dh1;
-        {
-          const f32x4 h1b1 = lds_read4(sH1T + tr + 16 * S_T);
-          f32x4 acc = zero4();
-#pragma unroll
-          for (int s2 = 0; s2 < KZ; ++s2) acc = mfma16(dz[s2], q2h[s2], acc);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[r] = (hreal_c[1] && h1b1[r] > 0.f) ? acc[r] : 0.f;
-          dh1 = acc;
-        }
-        f32x4 G1h[2] = {zero4(), zero4()};
-#pragma unroll
-        for (int s2 = 0; s2 < KB; ++s2) {
-          G1h[0] = mfma16(hc.b0[s2], dh1[s2], G1h[0]);
-          G1h[1] = mfma16(hc.b1[s2], dh1[s2], G1h[1]);
-        }
-        {
-          float dummy = 0.f;
-          float an[4] = {0.f, 0.f, 0.f, 0.f};
-          adam4<false>(P1[0], M1[0], V1[0], an, G1h[0], K, dummy);
-          adam4<false>(P1[1], M1[1], V1[1], an, G1h[1], K, dummy);
-        }
-        // ---- the next chunk's layer-1 partial, hidden tile 1 (stale after an
-        // epoch's last batch; unused)
-        l1h = l1h_partial(hn);
-        hc = hn;
-      }
-      if (g4_pending) apply_w4();   // the epoch's last W4 update, before validation
-      w1h_to_lds(P1);               // W1 rows 16..31 master (validation, snapshot)
-      if (epoch_tail(ep, 0.0, 0.0)) break;
-    }
-    // write back (barriers as the main branch; the mains stage to global)
-    __syncthreads();
-    __syncthreads();
-    w4_to_lds(M4, L);
-    w1h_to_lds(M1);
-    __syncthreads();
-    __syncthreads();
-    w4_to_lds(V4, L);
-    w1h_to_lds(V1);
-    __syncthreads();
-    return;
-  }
 
   if (helper) {
     // =========================== helper waves ===================================
@@ -972,13 +740,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   auto l1_partial = [&](const XChunk& x, f32x4& acc0, f32x4& acc1) {
     acc0 = zero4();
     acc1 = zero4();
-    if (SPL && !(FEDMX_HW_SPLIT_DEBUG & 3)) {   // hidden tile 1 is the helper's
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc0 = mfma16(P.q1[0][0][j], x.f0[j], acc0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc0 = mfma16(P.q1[0][1][j], x.f1[j], acc0);
-      return;
-    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       acc0 = mfma16(P.q1[0][0][j], x.f0[j], acc0);
@@ -1049,12 +810,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       {
         float* red = sRedH1 + parity * L_RED;
         lds_write4(red + (w * 2 + 0) * 256 + lane * 4, l1a);
-        if ((FEDMX_HW_SPLIT_DEBUG & 2) && ep == 0 && bi == 0 && blockIdx.x == 0 && A.stamps != nullptr) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) A.stamps[(w * 64 + lane) * 4 + r] = (uint64_t)__float_as_uint(l1b[r]);
-        }
-        if (!SPL || (FEDMX_HW_SPLIT_DEBUG & 1))
-          lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1b);   // SPLIT: the helper's slot
+        lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1b);
         HSTAMP(ms, 1);
         if (HWF) {
           flag_set(w, js + 1);        // (release: the partial writes above complete first)
@@ -1214,19 +970,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
       HSTAMP(ms, 7);
       f32x4 dh3[2];
-      f32x4 red8[2][4];
-      if (FEDMX_HW_RED8) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int ww = 0; ww < 4; ++ww) red8[t][ww] = lds_read4(sRedDH3 + (ww * 2 + t) * 256 + lane * 4);
-      }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        f32x4 s = FEDMX_HW_RED8 ? red8[t][0] : lds_read4(sRedDH3 + t * 256 + lane * 4);
+        f32x4 s = lds_read4(sRedDH3 + t * 256 + lane * 4);
 #pragma unroll
         for (int ww = 1; ww < 4; ++ww) {
-          const f32x4 o = FEDMX_HW_RED8 ? red8[t][ww] : lds_read4(sRedDH3 + (ww * 2 + t) * 256 + lane * 4);
+          const f32x4 o = lds_read4(sRedDH3 + (ww * 2 + t) * 256 + lane * 4);
 #pragma unroll
           for (int r = 0; r < 4; ++r) s[r] = s[r] + o[r];
         }
@@ -1255,7 +1004,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       for (int t = 0; t < 2; ++t) {
         h1b[t] = lds_read4(sH1T + tr + 16 * t * S_T);
         dh1b[t] = zero4();
-        if (SPL && t == 1) continue;   // hidden tile 1: the helper forms its dH1 itself
         f32x4 acc = zero4();
 #pragma unroll
         for (int s = 0; s < KZ; ++s) acc = mfma16(dz[s], q2[t][s], acc);
@@ -1265,23 +1013,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
       HSTAMP(ms, 8);
       // ---- dW1^T (own columns) = X^T dH1
-      constexpr bool PIPE = FEDMX_HW_PIPE && !PROX && !MULTI;
 #pragma unroll
       for (int s = 0; s < KB; ++s) {
-        if (SPL) {   // hidden tile 0 only
-          G1[0][0] = mfma16(cur.b0[s], dh1b[0][s], G1[0][0]);
-          G1[0][1] = mfma16(cur.b1[s], dh1b[0][s], G1[0][1]);
-        } else if (PIPE) {   // the v = 0 quads' gradients complete first
-          G1[0][0] = mfma16(cur.b0[s], dh1b[0][s], G1[0][0]);
-          G1[1][0] = mfma16(cur.b0[s], dh1b[1][s], G1[1][0]);
-          G1[0][1] = mfma16(cur.b1[s], dh1b[0][s], G1[0][1]);
-          G1[1][1] = mfma16(cur.b1[s], dh1b[1][s], G1[1][1]);
-        } else {
-          G1[0][0] = mfma16(cur.b0[s], dh1b[0][s], G1[0][0]);
-          G1[0][1] = mfma16(cur.b1[s], dh1b[0][s], G1[0][1]);
-          G1[1][0] = mfma16(cur.b0[s], dh1b[1][s], G1[1][0]);
-          G1[1][1] = mfma16(cur.b1[s], dh1b[1][s], G1[1][1]);
-        }
+        G1[0][0] = mfma16(cur.b0[s], dh1b[0][s], G1[0][0]);
+        G1[0][1] = mfma16(cur.b1[s], dh1b[0][s], G1[0][1]);
+        G1[1][0] = mfma16(cur.b0[s], dh1b[1][s], G1[1][0]);
+        G1[1][1] = mfma16(cur.b1[s], dh1b[1][s], G1[1][1]);
       }
       wave_sync();
       // ---- owned small tile: w<2 -> dW3 tile = dH3^T Z ; w>=2 -> dW2 tile = dZ^T H1
@@ -1303,32 +1040,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           adam4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
         }
       };
-      if (PIPE) {
-        // Adam(v = 0 quads) -> their 8 layer-1 MFMAs, with Adam(v = 1 quads)
-        // issued between them -> the remaining 8 MFMAs
-        finalize_chunk(nxt);
-        adam_w1(0, 0);
-        adam_w1(1, 0);
-        l1a = zero4();
-        l1b = zero4();
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          l1a = mfma16(P.q1[0][0][j], nxt.f0[j], l1a);
-          l1b = mfma16(P.q1[1][0][j], nxt.f0[j], l1b);
-        }
-        adam_w1(0, 1);
-        adam_w1(1, 1);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          l1a = mfma16(P.q1[0][1][j], nxt.f1[j], l1a);
-          l1b = mfma16(P.q1[1][1][j], nxt.f1[j], l1b);
-        }
-      } else {
+      {
         // W1 first: the next chunk's layer-1 product waits on it
         // (MULTI: the batch's last chunk only)
         if (last_ch) {
 #pragma unroll
-          for (int t = 0; t < (SPL ? 1 : 2); ++t)
+          for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int v = 0; v < 2; ++v) adam_w1(t, v);
         }
@@ -1353,7 +1070,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #endif
       cur = nxt;
     }
-    w1_to_lds(P, L, SPL ? 1 : 2);   // W1 master (validation, snapshot; SPLIT: rows 16..31 are the helper's)
+    w1_to_lds(P, L);   // W1 master (validation, snapshot)
     double prox_now = 0.0;
     if (PROX) {
       float pr = 0.f;
@@ -1381,12 +1098,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   __syncthreads();
   masters_to_global_o<CP>(Pg, sW1, sW4, sW2, sW3);
   __syncthreads();
-  w1_to_lds(M, L, SPL ? 1 : 2);
+  w1_to_lds(M, L);
   own_to_lds(M, L);
   __syncthreads();
   masters_to_global_o<CP>(Mg, sW1, sW4, sW2, sW3);
   __syncthreads();
-  w1_to_lds(V, L, SPL ? 1 : 2);
+  w1_to_lds(V, L);
   own_to_lds(V, L);
   __syncthreads();
   masters_to_global_o<CP>(Vg, sW1, sW4, sW2, sW3);

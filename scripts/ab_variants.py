@@ -22,20 +22,16 @@ VARIANTS = {
     # helper delays hd8/16/24, priorities hprio1/3 and (r2) hwprio1/3: all measured slower or
     # neutral (profiles/r3_train_hw_experiments.md); their switches were removed from the kernel
     # (source in git history, commit 5365856)
+    # r4: pipelined W1 Adam (pipe, flags_pipe, flags2_pipe), the SPLIT step (hwsplit,
+    # hwsplitd1/2) and grouped dH3 reads (red8) measured slower and were removed from
+    # the kernel (profiles/r4_train_hw_experiments.md; source in git history, commit ef22669)
     "exact": ["-DFEDMX_EXACT_ADAM=1"],               # r4: IEEE sqrt / division Adam (torch's op sequence)
     "flags": ["-DFEDMX_HW_FLAGS=1"],                 # r4: mains-only layer-1 exchange + helper->main LDS flags
     "flags_madam": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=32"],   # timing only: + mains skip W1 Adam
     "flags_hnone": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=64"],   # timing only: + helpers idle
-    "pipe": ["-DFEDMX_HW_PIPE=1"],                   # r4: W1 Adam / next layer-1 software-pipelined by half-tile
-    "flags_pipe": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_PIPE=1"],
-    "hwsplit": ["-DFEDMX_HW_SPLIT=1"],               # r4: layer-1 hidden tile 1 + its backward / Adam on the helpers
     "noiglp": ["-DFEDMX_HW_IGLP=-1"],               # r4: no iglp_opt hint in the step loop
     "iglp1": ["-DFEDMX_HW_IGLP=1"],                 # r4: iglp_opt(1) in the step loop
-    "red8": ["-DFEDMX_HW_RED8=1"],                   # r4: dH3 partial reads issued together (the ISA co-simulation predicts -4.6 %)
-    "hwsplitd1": ["-DFEDMX_HW_SPLIT=1", "-DFEDMX_HW_SPLIT_DEBUG=1"],   # diagnosis only
-    "hwsplitd2": ["-DFEDMX_HW_SPLIT=1", "-DFEDMX_HW_SPLIT_DEBUG=2"],   # diagnosis only
     "flags2": ["-DFEDMX_HW_FLAGS=2"],                # r4: no workgroup barrier in the step loop
-    "flags2_pipe": ["-DFEDMX_HW_FLAGS=2", "-DFEDMX_HW_PIPE=1"],
     "packed": ["-DFEDMX_HW_PACKED=1"],               # packed-fp32 Adam (bit-identical)  966-974 vs 948-951 (+2 %)
     "abl_pf": ["-DFEDMX_HW_ABLATE=8"],               # timing only: prefetch always hits the cache
     "abl_hadam": ["-DFEDMX_HW_ABLATE=16"],           # timing only: helpers skip W4's Adam
