@@ -239,3 +239,14 @@ def test_isa_timeline_on_a_tiny_listing(tmp_path):
     assert lp and lp[0]["mfma"] == 1 and lp[0]["barriers"] == 2
     ws = T.cosim([T.parse(lines[lp[0]["start"]:lp[0]["end"] + 1])] * 2, ["a", "b"], iters=3)
     assert all(w.iters == 3 for w in ws)
+    # no VALU / MFMA co-execution (--mfma-hold 32, profiles/r4_step_isa_timeline.md):
+    # the other wave's VALU waits out the whole MFMA
+    pair = [T.parse(["\tv_mfma_f32_16x16x4_f32 v[4:7], v0, v1, v[4:7]", "\ts_cbranch_scc1 .LBB0_1"]),
+            T.parse(["\tv_add_f32_e32 v9, v10, v11", "\ts_cbranch_scc1 .LBB0_1"])]
+    old_hold = T.MFMA_VPORT_HOLD
+    try:
+        T.MFMA_VPORT_HOLD = 32
+        a, b = T.cosim(pair, ["mfma", "valu"], iters=2)
+        assert b.stall["vector port (other wave)"] >= 28
+    finally:
+        T.MFMA_VPORT_HOLD = old_hold
