@@ -70,7 +70,8 @@
 // probe; profiles/r4_train_hw_experiments.md, source in git history before
 // this note.)
 #ifndef FEDMX_HW_IGLP
-#define FEDMX_HW_IGLP 0   // the step loop's iglp_opt strategy (-1: none; r4 A/B: +12.6 %, 1: +1.6 %)
+#define FEDMX_HW_IGLP 0   // the step loop's iglp_opt strategy (-1: none; r4 A/B: +12.6 %, 1: +1.6 %;
+                          // a second hint in the forward segment or the helpers' step: neutral)
 #endif
 // bound on one flag wait (polls); a wait that runs out marks the launch failed
 // (epochs_run = -1000) instead of hanging the GPU
