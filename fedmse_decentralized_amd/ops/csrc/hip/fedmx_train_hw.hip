@@ -69,15 +69,6 @@
 // partial reads issued together (+6.5 %, LDS issue stalls) and a co-simulation
 // probe; profiles/r4_train_hw_experiments.md, source in git history before
 // this note.)
-// 1: the epoch's Adam scalars (f64 bias corrections, -lr/bc1, sqrt(bc2) and
-// its reciprocal) as one LDS table built at the epoch start by one helper,
-// one lane per step (the same f64 recurrence and operations: bit-identical),
-// instead of every helper forming the next step's scalars (~25 f64 / f32
-// division and square-root instructions per step on every SIMD).  Barrier
-// hand-off only, epochs of <= 64 Adam steps (else the per-step path).
-#ifndef FEDMX_HW_KTAB
-#define FEDMX_HW_KTAB 0
-#endif
 #ifndef FEDMX_HW_IGLP
 #define FEDMX_HW_IGLP 0   // the step loop's iglp_opt strategy (-1: none; r4 A/B: +12.6 %, 1: +1.6 %;
                           // a second hint in the forward segment or the helpers' step: neutral)
@@ -120,8 +111,7 @@ constexpr int L_T32 = 32 * S_T;          // 640
 constexpr int L_T16 = 16 * S_T;          // 320
 constexpr int L_SCR = 4 * L_T32 + 2 * L_T16;  // 3200 per main wave (dY^T, H3^T, H1^T, dH3^T | Z^T, dZ^T)
 constexpr int L_Q4 = 4 * 4 * 64 * 4;     // 4096 W4 rows in the dH3 A-operand layout [w][v][t][lane][4]
-constexpr int L_KT = FEDMX_HW_KTAB ? 64 * 4 : 0;   // per-epoch Adam-scalar table (FEDMX_HW_KTAB)
-constexpr int L_TOTAL = L_W1 + L_W4 + L_W2 + L_W3 + 3 * L_RED + 4 * L_SCR + L_Q4 + 128 + L_KT;
+constexpr int L_TOTAL = L_W1 + L_W4 + L_W2 + L_W3 + 3 * L_RED + 4 * L_SCR + L_Q4 + 128;
 static_assert(L_TOTAL * 4 <= 160 * 1024, "LDS budget");
 
 // main-wave optimizer state: W1 column block (MFMA A-operand layout) + small tile
@@ -243,10 +233,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // [4..7] W4 / Adam scalars for step count v published by helper w;
   // [8..11] (FLAGS 2) dH3 partial + dY^T / H3^T of step count v written by main w
   int* const sFlag = reinterpret_cast<int*>(sK + 32);
-#if FEDMX_HW_KTAB
-  // KTAB: [64][neg_step_size, inv_bc2s, bc2s, -] of the epoch's Adam steps
-  float* const sKT = reinterpret_cast<float*>(sFlag + 16);
-#endif
   bool spin_fail = false;
   auto flag_set = [&](int i, int v) {
     if (lane == 0) __hip_atomic_store(sFlag + i, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -511,29 +497,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   K.two_mu = 2.f * A.mu;
   double b1pow = pow((double)A.beta1, (double)step);
   double b2pow = pow((double)A.beta2, (double)step);
-  // KTAB (see FEDMX_HW_KTAB): this epoch's nb Adam steps, lane i holding step
-  // i's scalars; lane i's powers take i + 1 multiplications of the running
-  // recurrence, which then continues from the epoch's last step
-  const bool ktab = FEDMX_HW_KTAB && !HWF && nb <= 64;
-#if FEDMX_HW_KTAB
-  auto build_ktab = [&]() {
-    double p1 = b1pow, p2 = b2pow;
-    for (int j = 0; j < nb; ++j)
-      if (j <= lane) {
-        p1 *= (double)A.beta1;
-        p2 *= (double)A.beta2;
-      }
-    if (lane < nb) {
-      const float ns = (float)(-((double)A.lr / (1.0 - p1)));
-      const float bc2s = (float)sqrt(1.0 - p2);
-      lds_write4(sKT + 4 * lane, f32x4{ns, 1.0f / bc2s, bc2s, 0.f});
-    }
-    b1pow = __shfl(p1, nb - 1);
-    b2pow = __shfl(p2, nb - 1);
-  };
-#else
-  auto build_ktab = [&]() {};
-#endif
   auto next_constants = [&]() {
     b1pow *= (double)A.beta1;
     b2pow *= (double)A.beta2;
@@ -651,19 +614,15 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         lds_write4(sK + 4 * (js & 1), f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f});
       }
     };
-    if (!ktab) publish_k();   // step 0's
+    publish_k();   // step 0's
     if (HWF) flag_set(4 + w, 1);   // W4 / scalars of launch step 0 published
     for (int ep = 0; ep < A.epochs; ++ep) {
       double acc_tr = 0.0;
-      if (ktab && w8 == 4) build_ktab();   // read after this epoch's first barrier
       // W4 gradient + Adam between barrier #2 of step s and barrier #1 of s+1
       int mb = 0, mch = 0;   // MULTI: batch / chunk of this step
       f32x4 G4[2][2];
       for (int bi = 0; bi < nsteps; ++bi) {
         const bool hs = (ep == 0 && bi == STAMP_STEP);
-#if FEDMX_HW_KTAB
-        const int kb = MULTI ? mb : bi;   // this step's Adam step within the epoch
-#endif
         const int nch = MULTI ? (min(B, n_tr - mb * B) + 15) / 16 : 1;
         const bool first_ch = !MULTI || mch == 0;
         const bool last_ch = !MULTI || mch + 1 == nch;
@@ -693,14 +652,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         const f32x4 w4a1 = lds_read4(sT0 + tr + 16 * S_T);
         const f32x4 w4b0 = lds_read4(sT1 + tr);
         const f32x4 w4b1 = lds_read4(sT1 + tr + 16 * S_T);
-#if FEDMX_HW_KTAB
-        if (ktab && last_ch) {   // this step's scalars, in flight with the dW4 operands
-          const f32x4 kk = lds_read4(sKT + 4 * kb);
-          K.neg_step_size = kk[0];
-          K.inv_bc2s = kk[1];
-          K.bc2s = kk[2];
-        }
-#endif
         if (first_ch) {
 #pragma unroll
           for (int v = 0; v < 2; ++v)
@@ -738,7 +689,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         w4_to_lds(P4, L);
         publish_q4();
         ++js;
-        if (!ktab) publish_k();   // step js's scalars, read by the mains after its barrier #1
+        publish_k();   // step js's scalars, read by the mains after its barrier #1
         if (HWF) flag_set(4 + w, js + 1);   // W4(js) ready for main w's layer 4
         HSTAMP(hs, 11);
       }
@@ -826,9 +777,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     for (int bi = 0; bi < nsteps; ++bi) {
       // MULTI: this step is chunk mch of batch mb (16 rows from row_b); the
       // batch's row count bt sets the scales, the chunk's bc the masks
-#if FEDMX_HW_KTAB
-      const int kb = MULTI ? mb : bi;   // this step's Adam step within the epoch (KTAB)
-#endif
       const int row_b = MULTI ? mb * B + 16 * mch : bi * B;
       const int bt = MULTI ? min(B, n_tr - mb * B) : min(B, n_tr - row_b);
       const int nch = MULTI ? (bt + 15) / 16 : 1;
@@ -875,11 +823,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         HSTAMP(ms, 2);
         auto read_helper_state = [&]() {
           // this step's Adam scalars (helper-published)
-#if FEDMX_HW_KTAB
-          const f32x4 kk = lds_read4(ktab ? sKT + 4 * kb : W4FLAG ? sK + 8 * w + 4 * (js & 1) : sK + 4 * (js & 1));
-#else
           const f32x4 kk = lds_read4(W4FLAG ? sK + 8 * w + 4 * (js & 1) : sK + 4 * (js & 1));
-#endif
           K.neg_step_size = kk[0];
           K.inv_bc2s = kk[1];
           K.bc2s = kk[2];

@@ -29,7 +29,7 @@ VARIANTS = {
     "flags": ["-DFEDMX_HW_FLAGS=1"],                 # r4: mains-only layer-1 exchange + helper->main LDS flags
     "flags_madam": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=32"],   # timing only: + mains skip W1 Adam
     "flags_hnone": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=64"],   # timing only: + helpers idle
-    "ktab": ["-DFEDMX_HW_KTAB=1"],                  # r4: per-epoch Adam-scalar table instead of per-step f64 math on every helper
+    # r4: per-epoch Adam-scalar table (ktab): +1.0 %, removed (commit 96da3e2)
     "noiglp": ["-DFEDMX_HW_IGLP=-1"],               # r4: no iglp_opt hint in the step loop
     "iglp1": ["-DFEDMX_HW_IGLP=1"],                 # r4: iglp_opt(1) in the step loop
     "flags2": ["-DFEDMX_HW_FLAGS=2"],                # r4: no workgroup barrier in the step loop
