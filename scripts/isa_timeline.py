@@ -13,7 +13,10 @@ counter that was last to arrive.
 
 Latency model (cycles; `/opt/skills/guides/MI355X_MICROARCH.md` constants
 table): `v_mfma_f32_16x16x4_f32` holds the matrix pipe 32 and the vector
-issue 8, dependent result 40; VALU issue 4 (transcendental 8, f64 8),
+issue 8 (the bf16 figure; for this fp32 MFMA the PMC counters show no VALU
+co-execution at all, `SQ_VALU_MFMA_COEXEC_CYCLES` = 0: use `--mfma-hold 32`,
+with which the co-simulated training step matches the measured one,
+profiles/r4_step_isa_timeline.md), dependent result 40; VALU issue 4 (transcendental 8, f64 8),
 result 8; `ds_read*` 64 (+16 for b128), `ds_write` 4 issue; LDS returns in
 order (`lgkmcnt`); global loads 500 (L2 / MALL resident chunks); SALU 2;
 `s_nop N` 4(N+1); `s_barrier` releases at its issue (the other waves are not
@@ -23,7 +26,7 @@ is not modelled either: its MFMAs and VALU compete for the same issue slots,
 so the simulated step is a lower bound for the wave's own chain.
 
   hipcc ... -gline-tables-only --cuda-device-only -S fedmx_train_hw.hip -o k.s
-  python scripts/isa_timeline.py k.s --kernel train_kernel_hwILb0 --loop auto
+  python scripts/isa_timeline.py k.s --kernel train_kernel_hwILb0ELb0 --cosim --mfma-hold 32 --lds-bw 64 --lds-queue 16
 """
 from __future__ import annotations
 
