@@ -395,6 +395,20 @@ def main(argv=None) -> int:
         span = seg[-1]["issue"] - (seg[0]["issue"] - seg[0]["stall"])
         print(f"  instr {s0:4d}-{s1 - 1:4d}: {span:6d} cycles, {sum(r['kind'] == 'mfma' for r in seg):3d} MFMA, "
               f"stall {sum(r['stall'] for r in seg):6d}")
+    # SIMD issue work (what an issue-bound step is made of): MFMA x hold +
+    # VALU issue cycles, per barrier segment and per source line
+    def work(r):
+        k, cost, _ = classify(r["op"])
+        return MFMA_PIPE[r["op"]][0] if k == "mfma" and MFMA_VPORT_HOLD >= 32 else (cost if k in ("mfma", "valu") else 0)
+    print(f"SIMD issue work of this wave (MFMA hold {MFMA_VPORT_HOLD}): {sum(work(r) for r in rows)} cycles; by segment: " +
+          ", ".join(str(sum(work(r) for r in rows[s0:s1])) for s0, s1 in zip(seg_edges[:-1], seg_edges[1:])))
+    by_work = collections.Counter()
+    for r in rows:
+        if r["loc"]:
+            by_work[(files.get(r["loc"][0], r["loc"][0]), r["loc"][1])] += work(r)
+    print(f"top {a.top} source lines by SIMD issue work:")
+    for (f, ln), v in by_work.most_common(a.top):
+        print(f"  {f}:{ln:<5d} {v:6d}")
     by_loc = collections.Counter()
     for r in rows:
         if r["stall"] and r["loc"]:
