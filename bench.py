@@ -109,14 +109,46 @@ def _spawn_ranks(n: int, argv) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+# transport probe outcome of this rank (parallel/probe.py): the record's
+# ``transport_fallback`` when the requested transport did not work
+_TRANSPORT = {"used": None, "fallback": None}
+
+
+def _probe_wanted(known) -> bool:
+    """A torch.distributed.run rank of a GPU job (FEDMX_BENCH_PROBE=1 forces
+    the probe on the CPU too, =0 skips it).  device_count() does not start
+    the HIP runtime."""
+    flag = os.environ.get("FEDMX_BENCH_PROBE", "auto")
+    if flag == "0" or int(os.environ.get("WORLD_SIZE", "1")) <= 1 or known.phantom_ranks > 1:
+        return False
+    if "TORCHELASTIC_USE_AGENT_STORE" not in os.environ:   # no launcher store to agree through
+        return False
+    return flag == "1" or torch.cuda.device_count() > 0
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
+    from fedmse_decentralized_amd.parallel import probe
+
+    if argv[:1] == [probe.PROBE_FLAG]:   # a probe child (parallel/probe.py)
+        return probe.child_main(argv[1])
     pre = argparse.ArgumentParser(add_help=False)
     pre.add_argument("--gpus", type=int, default=1)
     pre.add_argument("--phantom-ranks", type=int, default=0)
+    pre.add_argument("--comm", default=None)
     known, _ = pre.parse_known_args(argv)
     if known.gpus > 1 and "WORLD_SIZE" not in os.environ and known.phantom_ranks <= 1:
         return _spawn_ranks(known.gpus, argv)
+    if _probe_wanted(known):
+        # before this process touches the GPU: the first transport that works
+        # on every rank (RCCL, else peer-memory IPC, else gloo)
+        requested = known.comm or os.environ.get("FEDMX_COMM") or "rccl"
+        used, fb = probe.choose_transport(os.path.abspath(__file__), requested,
+                                          timeout_s=float(os.environ.get("FEDMX_PROBE_TIMEOUT_S", "180")))
+        os.environ.update(probe.TRANSPORT_ENV[used])
+        _TRANSPORT["used"], _TRANSPORT["fallback"] = used, fb
+        if fb is not None and os.environ.get("RANK") == "0":
+            print(f"transport fallback: {requested} -> {used}: {fb['failures']}", file=sys.stderr)
     # stdout carries exactly ONE line, the JSON record: native libraries'
     # chatter (RCCL prints a version banner to stdout when a communicator is
     # created) is routed to stderr for the duration of the run
@@ -209,7 +241,8 @@ def _auc(last, fed=None, phantom=False):
     m = np.asarray(last.metrics, dtype=np.float64)
     if phantom and fed is not None and fed.local:
         m = m[fed.local[0]:fed.local[-1] + 1]
-    return float(np.mean(m)), float(np.min(m))
+    m = m[~np.isnan(m)]   # (a client without abnormal test rows has no AUC)
+    return (float(np.mean(m)), float(np.min(m))) if m.size else (float("nan"), float("nan"))
 
 
 def _extra_fields(rec, build, fed, comm, device, args, n_gpus, dt, auc, auc_min):
@@ -306,7 +339,8 @@ def _main(argv, real_stdout: int):
 
         comm = PhantomComm(args.phantom_ranks, device)
     else:
-        comm = init_comm(device=device, comm_impl=args.comm)
+        # (a probed job: the transport the probe settled on, exported in FEDMX_COMM)
+        comm = init_comm(device=device, comm_impl=None if _TRANSPORT["used"] else args.comm)
     setup_logging("WARNING", rank=comm.rank)
     n_gpus = comm.world_size
     if args.gpus != n_gpus and comm.is_root:
@@ -389,6 +423,10 @@ def _main(argv, real_stdout: int):
             "timed_ms": round(1e3 * dt, 3),
             "writer_busy_ms_per_round": round(1e3 * fed.writer.busy_s_timed / args.steps, 4),
         }
+        if _TRANSPORT["used"] is not None:
+            rec["config"]["transport"] = _TRANSPORT["used"]
+        if _TRANSPORT["fallback"] is not None:
+            rec["transport_fallback"] = _TRANSPORT["fallback"]
         if train_ms is not None:
             t = train_ms                       # [ranks, timed rounds], 0 = no local selection
             own = t[t > 0]
@@ -407,20 +445,44 @@ def _main(argv, real_stdout: int):
             rec["detection_auc_scope"] = "rank-0 clients only"
             rec["projection"] = (f"rank 0 of a {args.phantom_ranks}-rank job on ONE GPU, collectives stubbed "
                                  "(no RCCL time); projected_value assumes every rank is as fast as this one")
+    def emit(r):
+        line = json.dumps(r)
+        os.write(real_stdout, (line + "\n").encode())
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
+
     if n_gpus > 1 and not phantom and not args.no_extra:
         fed.finish()
+        # The headline must not depend on the extras: a rank that raises in
+        # them leaves the others blocked in a collective.  Every rank arms a
+        # watchdog; when it fires, rank 0 prints the headline (marked) and
+        # every rank leaves, so the launcher sees the job end.
+        import threading
+
+        limit = float(os.environ.get("FEDMX_BENCH_EXTRA_TIMEOUT_S", "600"))
+
+        def _give_up():
+            if rec is not None:
+                rec["extra_fields_error"] = f"extras did not finish within {limit:.0f} s (a rank failed or hung)"
+                emit(rec)
+            print(f"rank {comm.rank}: extra measurements timed out; exiting", file=sys.stderr, flush=True)
+            os._exit(0)
+
+        watchdog = threading.Timer(limit, _give_up)
+        watchdog.daemon = True
+        watchdog.start()
         try:
+            if os.environ.get("FEDMX_BENCH_TEST_STALL_RANK") == str(comm.rank):   # tests: a stuck rank
+                time.sleep(3600)
             _extra_fields(rec, build, fed, comm, device, args, n_gpus, dt, auc, auc_min)
         except Exception as e:   # the headline stands on its own: record why the extras are missing
             print(f"rank {comm.rank}: extra measurements failed: {e!r}", file=sys.stderr)
             if rec is not None:
                 rec["extra_fields_error"] = repr(e)[:300]
+        watchdog.cancel()
     if rec is not None:
-        line = json.dumps(rec)
-        os.write(real_stdout, (line + "\n").encode())
-        if args.out:
-            with open(args.out, "w") as f:
-                f.write(line + "\n")
+        emit(rec)
     fed.writer.report_stats()   # FEDMX_WRITER_STATS=1: per-job writer times on stderr
     shutdown(comm)
     return 0

@@ -153,6 +153,13 @@ class ExperimentConfig:
         return os.path.join(self.output_root, f"Checkpoint/{self.network_size}/{self.experiment_name}/{run}/ClientModel",
                             self.scen_name, model_type, update_type, device_name)
 
+    def __post_init__(self):
+        # fixed-mode-only options (the reference's rules otherwise): the
+        # relative drift rule replaces model_verifier.py:72-75's absolute 3.0
+        if self.drift_threshold_rel > 0 and self.compat != "fixed":
+            raise ValueError("drift_threshold_rel > 0 replaces the reference's absolute drift rule "
+                             "(src/Trainer/model_verifier.py:72-75): it needs compat='fixed'")
+
     def resolved_init_mode(self) -> str:
         if self.init_mode == "auto":
             return "per_client" if self.compat == "reference" else "shared"
@@ -198,6 +205,10 @@ def add_arguments(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
             p.add_argument(name, type=int, default=None)
         elif isinstance(default, float):
             p.add_argument(name, type=float, default=None)
+        elif default is None and str(f.type) in ("Optional[float]", "float"):   # e.g. synthetic_alpha
+            p.add_argument(name, type=float, default=None)
+        elif default is None and str(f.type) in ("Optional[int]", "int"):
+            p.add_argument(name, type=int, default=None)
         else:
             p.add_argument(name, type=str, default=None)
     # reference spelling alias

@@ -235,6 +235,20 @@ class DeviceRound:
         self.elect_mode = (1 if cfg.election == "majority" else 0) | (6 if self.thesis else 0)
         self.centralized = cfg.aggregation_mode == "centralized"
         self.drift_rel = cfg.drift_threshold_rel > 0   # kernel mode 3: drift <= rel x ||history||
+        # training-failure word (TrainArgs.err): a launch whose bounded flag
+        # wait ran out sets it; the election kernel reads it and skips the
+        # round's aggregation and adoption (report ELECT_TRAIN_FAILED).  With
+        # collectives it is the last word of this rank's exchange records row,
+        # so it rides the all-gather and every rank sees every rank's failure.
+        self.err = torch.zeros(1, dtype=i32, device=dev)
+        self.err_ptr = self.err.data_ptr()
+        self.err_n, self.err_stride = 1, 0
+        if fed.comm.collective:
+            if 8 * self.xslots <= P_PAD - 4:   # the records (4 doubles per slot) end before it
+                self.err_ptr = self.xsend.data_ptr() + 4 * (P_PAD - 1)
+                self.xsend[0, P_PAD - 1] = 0.0   # int32 0
+            else:
+                self.err_n = 0   # (more than 1,150 clients on one rank: the host-side check only)
         self.pending: deque = deque()
         # optional: HIP-event time of every round's training launch (bench.py
         # at N > 1 measures the wait for the slowest rank's largest client)
@@ -340,9 +354,19 @@ class DeviceRound:
     def _loc(self, c):
         return c - self.start
 
+    def _check_failed(self, rec: dict) -> None:
+        if int(rec["report"][0]) == _hip.ELECT_TRAIN_FAILED:
+            raise RuntimeError(f"round {rec['round'] + 1}: a training launch failed (a wave's bounded flag wait "
+                               "ran out); the device skipped that round's aggregation and adoption")
+
     def enqueue(self, selected: List[int]) -> LazyRoundResult:
         fed = self.fed
         cfg, eng, st, comm = fed.cfg, fed.engine, fed.engine.store, fed.comm
+        # a pending round whose election already reported a failed training
+        # launch (mapped report slot, no synchronisation): stop before enqueueing more
+        for r in self.pending:
+            if "report" in r:
+                self._check_failed(r)
         tel = fed.tel
         N, dev = self.N, self.dev
         rnd = fed.round_idx
@@ -372,6 +396,7 @@ class DeviceRound:
             if self.train_timing and local_sel:
                 tev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 tev[0].record()
+            eng.train_err_ptr = self.err_ptr
             handle = eng.train_launch(local_rows, fed.hp) if local_sel else None
             if tev is not None:
                 tev[1].record()
@@ -457,6 +482,12 @@ class DeviceRound:
         with tel.phase("aggregate"):
             noise = np.asarray(fed.noise.rand_n(k * (k - 1)), dtype=np.float64)
             if comm.collective:
+                # every rank's failure word, read in place from the gathered records rows
+                err_ptr, err_n, err_stride = base.data_ptr() + 4 * (P_PAD - 1), self.err_n * comm.world_size, \
+                    (slots + 1) * P_PAD
+            else:
+                err_ptr, err_n, err_stride = self.err_ptr, self.err_n, 0
+            if comm.collective:
                 sel_ptr, noise_ptr, rows_ptr, rec_ptr = self.rt.desc.put(
                     np.asarray(selected, dtype=np.int32), noise if noise.size else np.zeros(1), rows, rec_idx)
                 vec_ptr = base.data_ptr()
@@ -485,7 +516,8 @@ class DeviceRound:
                                rule=self.rule, mode=self.elect_mode, rec=rec_ptr, hw=hw_ptr,
                                vote_cap=float(cfg.thesis_vote_mse_cap),
                                # thesis fallback: one uniform per round, drawn whatever the outcome
-                               fallback_u=fed.fallback_rng.random() if self.thesis else 0.0)
+                               fallback_u=fed.fallback_rng.random() if self.thesis else 0.0,
+                               err=err_ptr, err_n=err_n, err_stride=err_stride)
             w = _hip.WsumArgs(base=base.data_ptr(), rows=rows_ptr, weights=self.weights.data_ptr(),
                               state=self.state.data_ptr(), out=self.agg.data_ptr(), k=k, P=P_PAD)
             _hip.elect_wsum(a, w, dev)
@@ -608,6 +640,7 @@ class DeviceRound:
         N = self.N
         rnd = rec["round"]
         info = log.isEnabledFor(logging.INFO)
+        self._check_failed(rec)
         agg = int(rec["report"][0])
         aggregator = agg if agg >= 0 else None
         slot = rec["slot"]
@@ -681,7 +714,9 @@ class DeviceRound:
             fed.check_replicas(rnd, rec["selected"], aggregator, metrics)
         stop = False
         if cfg.global_early_stop:
-            stop = fed.early.update(float(np.min(metrics)))
+            from ..federation import metric_stats
+
+            stop = fed.early.update(metric_stats(metrics)[1])
         rec.update(aggregator=aggregator, metrics=metrics, verification=verification, epochs_run=epochs_local,
                    stop=stop, done=True)
         for key in ("handle", "snap_slot", "slot", "report", "_keep", "event", "eval_params", "eval_timing", "train_ev"):

@@ -61,8 +61,12 @@ class HipEngine(Engine):
         return out
 
     # -- training ------------------------------------------------------------------
+    # device address of an int32 the training kernel sets to 1 when a launch
+    # fails (engine/device_round.py points it at the round's error word)
+    train_err_ptr = 0
+
     def train_launch(self, local_ids: Sequence[int], hp: TrainHParams) -> TrainHandle:
-        trk, er, be = _hip.train(self.store, list(local_ids), hp, self.dims)
+        trk, er, be = _hip.train(self.store, list(local_ids), hp, self.dims, err=self.train_err_ptr)
         return TrainHandle(list(local_ids), [trk, er, be])
 
     def train_collect(self, handle: TrainHandle, host: Optional[List[np.ndarray]] = None) -> TrainResult:

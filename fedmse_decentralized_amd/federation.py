@@ -57,6 +57,29 @@ _PREP_CACHE: Dict[tuple, Tuple[List[ClientData], np.ndarray]] = {}
 # data
 # ----------------------------------------------------------------------------
 
+def _load_optional(path: str, n_cols: int, name: str) -> np.ndarray:
+    """A client's abnormal rows, or none: the shipped N-BaIoT non-IID split
+    lacks ``abnormal/`` for clients 6, 9 and 10 (`/root/reference/.MISSING_LARGE_BLOBS:4-6`).
+    Such a client trains, votes and verifies as usual; its test set holds
+    normal rows only, so its detection AUC is undefined: reported as null and
+    left out of every mean / min / max (io/reports.py, metric_stats)."""
+    try:
+        return load_data(path)
+    except FileNotFoundError:
+        log.warning(f"{name}: no abnormal data at {path}: AUC undefined for this client (reported as null)")
+        return np.zeros((0, n_cols), dtype=np.float64)
+
+
+def metric_stats(metrics) -> Tuple[float, float, float]:
+    """(mean, min, max) over the clients whose metric is defined (a client
+    without abnormal test rows has a NaN AUC); NaN when none is."""
+    m = np.asarray(metrics, dtype=np.float64)
+    m = m[~np.isnan(m)]
+    if m.size == 0:
+        return float("nan"), float("nan"), float("nan")
+    return float(m.mean()), float(m.min()), float(m.max())
+
+
 def load_federation_data(cfg: ExperimentConfig, py_rng: random.Random) -> Tuple[List[ClientData], np.ndarray]:
     """Device sampling + per-client preparation with the reference RNG order.
 
@@ -86,7 +109,7 @@ def load_federation_data(cfg: ExperimentConfig, py_rng: random.Random) -> Tuple[
         for d in chosen:
             log.info("Loading data from {}...".format(d.name))
             normal = load_data(dl.resolve(d.normal_data_path))
-            abnormal = load_data(dl.resolve(d.abnormal_data_path))
+            abnormal = _load_optional(dl.resolve(d.abnormal_data_path), normal.shape[1], d.name)
             if cfg.new_device:
                 if not d.test_normal_data_path:
                     raise ValueError(f"device {d.name} has no test_normal_data_path (needed with new_device)")
@@ -483,7 +506,7 @@ class Federation:
             self.check_replicas(rnd, selected, aggregator, metrics)
         stop = False
         if cfg.global_early_stop:
-            stop = self.early.update(float(np.min(metrics)))
+            stop = self.early.update(metric_stats(metrics)[1])
         self.round_idx += 1
         times = self.tel.end_round(round=rnd + 1, selected=len(selected), aggregator=aggregator)
         return RoundResult(rnd, list(selected), aggregator, metrics, verification_results, epochs_all, stop, times)
@@ -682,7 +705,7 @@ class Federation:
                 path = os.path.join(cfg.output_root, f"Checkpoint/LatentData/{cfg.network_size}/{cfg.experiment_name}/"
                                     f"Run_{self.run}/latent_{self.model_type}_{self.update_type}.pkl")
                 ckpt.save_latents(path, merged)
-        return float(np.max(self.last_metrics))
+        return metric_stats(self.last_metrics)[2]
 
     # -- resume ---------------------------------------------------------------------
     def snapshot(self) -> Dict:

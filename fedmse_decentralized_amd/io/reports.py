@@ -35,12 +35,17 @@ def _append_line(path: str, obj, files=None) -> None:
 def append_round_result(cfg, run: int, rnd: int, metrics: Sequence[float], model_type: str, update_type: str,
                         files=None) -> str:
     path = results_path(cfg, run, model_type, update_type)
+    # an undefined metric (NaN: a client with no abnormal test rows) is written
+    # as null and left out of global_loss (the reference would write NaN and
+    # take an order-dependent min)
+    vals = [None if s != s else float(s) for s in metrics]
+    defined = [v for v in vals if v is not None]
     _append_line(path, {
         "round": rnd + 1,
-        "client_metrics": [float(s) for s in metrics],
+        "client_metrics": vals,
         "update_type": update_type,
         "model_type": model_type,
-        "global_loss": min(metrics) if len(metrics) else float("inf"),
+        "global_loss": min(defined) if defined else (float("inf") if not len(metrics) else None),
     }, files)
     return path
 

@@ -35,6 +35,9 @@ TRAIN_COMPACT = os.environ.get("FEDMX_TRAIN_COMPACT", "1") != "0"
 TRAIN_FLAG_NO_COMPACT = 1
 TRAIN_FLAG_HELPER = 2
 TRAIN_FLAG_NO_HELPER = 4
+TRAIN_FLAG_TEST_DROP_W4 = 8   # tests only: inject a flag-wait timeout (fedmx_train_hw.hip)
+# extra TrainArgs.flags bits OR'd into every launch (tests/test_train_failure_gpu.py)
+TRAIN_TEST_FLAGS = 0
 # helper-wave training kernel (fedmx_train_hw.hip: 8 waves, W4's gradient and
 # Adam on a second wave per SIMD) for the compact shapes: "1" on, "0" off,
 # unset: the library's build default
@@ -73,6 +76,7 @@ class TrainArgs(ctypes.Structure):
         ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
         ("eps", ctypes.c_float), ("lam", ctypes.c_float), ("mu", ctypes.c_float),
         ("stamps", ctypes.c_void_p), ("flags", ctypes.c_int32), ("pad0", ctypes.c_int32),
+        ("err", ctypes.c_void_p),
     ]
 
 
@@ -82,7 +86,11 @@ _vp, _i32 = ctypes.c_void_p, ctypes.c_int32
 class ElectArgs(ctypes.Structure):
     _fields_ = [("sel", _vp), ("vec", _vp), ("noise", _vp), ("agg_counts", _vp), ("weights", _vp), ("state", _vp),
                 ("report", _vp), ("k", _i32), ("cap", _i32), ("rule", _i32), ("mode", _i32), ("rec", _vp),
-                ("hw", _vp), ("vote_cap", ctypes.c_double), ("fallback_u", ctypes.c_double)]
+                ("hw", _vp), ("vote_cap", ctypes.c_double), ("fallback_u", ctypes.c_double),
+                ("err", _vp), ("err_n", _i32), ("err_stride", _i32)]
+
+
+ELECT_TRAIN_FAILED = -3   # report[0] of a round whose training launch failed (TrainArgs.err set)
 
 
 class WsumArgs(ctypes.Structure):
@@ -713,7 +721,7 @@ class TrainBuffers:
 
 
 def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tensor] = None,
-          compact: Optional[bool] = None, helper: Optional[bool] = None):
+          compact: Optional[bool] = None, helper: Optional[bool] = None, err: int = 0):
     """Launch the fused training kernel for store rows ``local_ids`` (async).
     Returns host views (tracking[k, E, 2], epochs_run[k], best_epoch[k])
     written by the kernel, valid after the next stream sync."""
@@ -750,10 +758,12 @@ def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tens
     a.lr, a.beta1, a.beta2, a.eps = hp.lr, hp.beta1, hp.beta2, hp.eps
     a.lam, a.mu = hp.shrink_lambda, hp.fedprox_mu
     a.stamps = stamps.data_ptr() if stamps is not None else None
+    a.err = err or None
     a.flags = 0 if (TRAIN_COMPACT if compact is None else compact) else TRAIN_FLAG_NO_COMPACT
     helper_on = TRAIN_HELPER if helper is None else helper
     if helper_on is not None:
         a.flags |= TRAIN_FLAG_HELPER if helper_on else TRAIN_FLAG_NO_HELPER
+    a.flags |= TRAIN_TEST_FLAGS
     rc = lib().fedmx_train(ctypes.byref(a), k, rt.stream)
     if rc == -2:
         raise ValueError(f"fused training kernel needs batch_size >= 1, got {hp.batch_size}")

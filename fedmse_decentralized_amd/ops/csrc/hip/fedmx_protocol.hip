@@ -51,8 +51,19 @@ struct ElectArgs {
   const float* hw;         // rule 2: [k] weights (they depend on the selection only)
   double vote_cap;         // mode bit 1
   double fallback_u;       // mode bit 2: this round's uniform draw (host, every round)
+  const int32_t* err;      // or null: err_n training-failure words (TrainArgs.err), err_stride
+  int32_t err_n, err_stride;   // ints apart (one per rank: the exchange rows carry them); any
+                               // set -> no aggregator, report[0] = ELECT_TRAIN_FAILED
 };
-static_assert(sizeof(ElectArgs) == 104, "ElectArgs layout is shared with Python");
+static_assert(sizeof(ElectArgs) == 120, "ElectArgs layout is shared with Python");
+constexpr int32_t ELECT_TRAIN_FAILED = -3;
+
+__device__ __forceinline__ int train_failed(const ElectArgs& E) {
+  int f = 0;
+  if (E.err != nullptr)
+    for (int r = 0; r < E.err_n; ++r) f |= E.err[(size_t)r * E.err_stride];
+  return f;
+}
 
 struct WsumArgs {
   const float* base;       // row-major [*, P]
@@ -92,6 +103,8 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
       const int k = E.k;
       int c = -1, cnt = 0;
       double vs = 0.0, mse = 1.0;
+      // (loaded with the other inputs; checked once the election is formed)
+      const int failed = train_failed(E);
       if (lane < k) {
         c = E.sel[lane];
         const int ri = E.rec != nullptr ? E.rec[lane] : c;
@@ -162,6 +175,9 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
           voter = -1;
         }
       }
+      // a failed training launch: its clients' parameters are invalid, so
+      // nothing is aggregated or adopted this round (the host raises)
+      if (failed) agg = -1;
       if (lane == 0) s_agg = agg;
       if (agg >= 0) {
         if (E.rule == 1) {
@@ -181,7 +197,7 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
       if (blockIdx.x == 0 && lane == 0) {
         E.state[0] = agg;
         E.state[1] = voter;
-        E.report[0] = agg;
+        E.report[0] = failed ? ELECT_TRAIN_FAILED : agg;
         E.report[1] = voter;
       }
       if (blockIdx.x == 0 && agg >= 0 && lane < k) E.weights[lane] = s_w[lane];
@@ -240,6 +256,8 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
         voter = -1;
       }
     }
+    const int failed = train_failed(E);
+    if (failed) agg = -1;
     s_agg = agg;
     if (agg >= 0) {
       if (E.rule == 1) {
@@ -257,7 +275,7 @@ __global__ __launch_bounds__(256) void elect_wsum_kernel(const ElectArgs E, cons
     if (blockIdx.x == 0) {
       E.state[0] = agg;
       E.state[1] = voter;
-      E.report[0] = agg;
+      E.report[0] = failed ? ELECT_TRAIN_FAILED : agg;
       E.report[1] = voter;
       if (agg >= 0)
         for (int j = 0; j < E.k; ++j) E.weights[j] = s_w[j];

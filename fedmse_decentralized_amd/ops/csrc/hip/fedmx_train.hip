@@ -62,11 +62,17 @@
 #ifndef FEDMX_W4_POS
 #define FEDMX_W4_POS 0
 #endif
-// 1: scaled-moment Adam (adam4s, fedmx_train_common.h: 5 instead of 8 VALU
-// issues per parameter); 0: adam4.  Measured (r2): 1.096 vs 1.091 ms — the
-// step is bound by its dependent chain, not by VALU issue — so off by default.
+// 1: scaled-moment Adam (adam4s, fedmx_train_common.h: 7 instead of 10 VALU
+// issues per parameter); 0: adam4.  Measured (r2): 1.096 vs 1.091 ms here --
+// this kernel's step is bound by its dependent chain -- but the helper-wave
+// kernel (fedmx_train_hw.hip) is SIMD-issue bound and gains 3 % with it (r5),
+// so both use it by default (the two kernels stay bit-identical: the shared
+// adam_scaled_step / adam_moment_in_scale); the IEEE-Adam build does not.
 #ifndef FEDMX_ADAM_SCALED
-#define FEDMX_ADAM_SCALED 0
+#define FEDMX_ADAM_SCALED (!FEDMX_EXACT_ADAM)
+#endif
+#if FEDMX_ADAM_SCALED && FEDMX_EXACT_ADAM
+#error "FEDMX_ADAM_SCALED rounds differently from torch; the IEEE-Adam build needs FEDMX_ADAM_SCALED=0"
 #endif
 #if FEDMX_ADAM_SCALED
 #define FEDMX_ADAM4 adam4s
@@ -284,8 +290,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   // moment scales of the scaled-moment Adam (identity otherwise)
   const float c1 = 1.f - A.beta1, c2 = 1.f - A.beta2;
   if (FEDMX_ADAM_SCALED) {
-    scale_slab(M, (float)(1.0 / (double)c1));
-    scale_slab(V, (float)(1.0 / (double)c2));
+    scale_slab(M, adam_moment_in_scale(A.beta1));
+    scale_slab(V, adam_moment_in_scale(A.beta2));
   }
   if (PROX) {
     global_to_masters_o<CP>(A.anchor + (size_t)cid * P_PAD, sW1, sW4, sW2, sW3);
@@ -619,6 +625,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   // beta^step as running products (python: 1 - beta ** step)
   double b1pow = pow((double)A.beta1, (double)step);
   double b2pow = pow((double)A.beta2, (double)step);
+  const AdamScaledInit KI = adam_scaled_init(A.lr, A.beta1, A.beta2, A.eps);
 
   double min_valid = __builtin_huge_val();
   int worse = 0, ep_run = 0, best_ep = -1;
@@ -666,13 +673,12 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         // 1 - beta ** step), computed at the batch start, off the critical path
         b1pow *= (double)A.beta1;
         b2pow *= (double)A.beta2;
-        K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
-        K.bc2s = (float)sqrt(1.0 - b2pow);
-        K.inv_bc2s = 1.0f / K.bc2s;
         if (FEDMX_ADAM_SCALED) {
-          const double S = -((double)A.lr / (1.0 - b1pow)) * (double)c1;
-          K.kd = (float)(sqrt((double)c2) / (sqrt(1.0 - b2pow) * S));
-          K.ed = (float)((double)A.eps / S);
+          adam_scaled_step(K, KI, b1pow, b2pow);
+        } else {
+          K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
+          K.bc2s = (float)sqrt(1.0 - b2pow);
+          K.inv_bc2s = 1.0f / K.bc2s;
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t)

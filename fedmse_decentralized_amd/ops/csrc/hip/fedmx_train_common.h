@@ -16,6 +16,9 @@
 #ifndef FEDMX_ADAM_FMA
 #define FEDMX_ADAM_FMA 1
 #endif
+#if FEDMX_EXACT_ADAM && !FEDMX_ADAM_FMA
+#error "FEDMX_EXACT_ADAM follows torch's fused lerp/addcmul: it needs FEDMX_ADAM_FMA=1"
+#endif
 
 namespace fedmx {
 
@@ -39,10 +42,15 @@ struct TrainArgs {
   uint64_t* stamps;         // [8 waves][32] s_memtime stamps of one step (FEDMX_STAMPS builds), or null
   int32_t flags;            // TRAIN_FLAG_* bits
   int32_t pad0;
+  int32_t* err;             // or null: set to 1 by a launch that failed (a flag wait ran out,
+                            // fedmx_train_hw.hip); read by elect_wsum_kernel, which then skips
+                            // the round's aggregation and adoption (engine/device_round.py)
 };
 constexpr int32_t TRAIN_FLAG_NO_COMPACT = 1;  // identity-order kernels even where the compact order applies
 constexpr int32_t TRAIN_FLAG_HELPER = 2;      // helper-wave kernel (fedmx_train_hw.hip) for the compact shapes
 constexpr int32_t TRAIN_FLAG_NO_HELPER = 4;   // never the helper-wave kernel
+constexpr int32_t TRAIN_FLAG_TEST_DROP_W4 = 8;   // tests only: one W4 hand-off is never published (a
+                                                 // flag-wait timeout in the FedProx helper-wave kernel)
 
 // In-kernel phase timestamps (build with -DFEDMX_STAMPS=1): wave w's lane 0 of
 // workgroup 0 records s_memtime at fixed points of training step STAMP_STEP
@@ -109,6 +117,27 @@ __device__ __forceinline__ void adam4s(float (&p)[4], float (&m)[4], float (&v)[
 #pragma unroll
   for (int r = 0; r < 4; ++r) p[r] = __builtin_fmaf(m[r], t0[r], p[r]);
 }
+
+// adam4s's per-step scalars (both training kernels, so the helper-wave and
+// the 4-wave kernels stay bit-identical): with 1/S = (b1^t - 1) / (lr (1-b1))
+//   ed = eps / S,  kd = sqrt(1-b2) / (sqrt(bc2) S) = sqrt(1-b2) (1/S) rsqrt(bc2)
+// -- only 1/S changes linearly per step: no f64 division or square root on
+// the step's path (the f32 rsqrt of bc2 is <= 1 ulp)
+struct AdamScaledInit {
+  double r_lrc1;   // 1 / (lr (1 - b1))
+  double sq_c2;    // sqrt(1 - b2)
+  double eps;
+};
+__device__ __forceinline__ AdamScaledInit adam_scaled_init(float lr, float beta1, float beta2, float eps) {
+  return AdamScaledInit{1.0 / ((double)lr * (double)(1.f - beta1)), sqrt((double)(1.f - beta2)), (double)eps};
+}
+__device__ __forceinline__ void adam_scaled_step(AdamStep& K, const AdamScaledInit& I, double b1pow, double b2pow) {
+  const double inv_s = (b1pow - 1.0) * I.r_lrc1;
+  K.ed = (float)(I.eps * inv_s);
+  K.kd = (float)(I.sq_c2 * inv_s) * __builtin_amdgcn_rsqf((float)(1.0 - b2pow));
+}
+// moment scale on load (m / (1-b1), v / (1-b2)); the write-back multiplies by 1-b
+__device__ __forceinline__ float adam_moment_in_scale(float beta) { return (float)(1.0 / (double)(1.f - beta)); }
 
 // torch.optim.Adam single-tensor update (no weight decay / amsgrad):
 //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2)

@@ -5,9 +5,18 @@
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"
-OUT=$ROOT/gpurun_out/ab
+OUT=${OUTAB:-$ROOT/gpurun_out/ab}
 mkdir -p "$OUT"
-LIBS=$(ls fedmse_decentralized_amd/ops/lib/libfedmx_hip_*.so | grep -v stamps)
+# AB_LIBS="base hwscaled0 ...": only these variants ("main" = the production libfedmx_hip.so)
+if [ -n "${AB_LIBS:-}" ]; then
+  LIBS=""
+  for n in $AB_LIBS; do
+    if [ "$n" = main ]; then LIBS="$LIBS fedmse_decentralized_amd/ops/lib/libfedmx_hip.so";
+    else LIBS="$LIBS fedmse_decentralized_amd/ops/lib/libfedmx_hip_$n.so"; fi
+  done
+else
+  LIBS=$(ls fedmse_decentralized_amd/ops/lib/libfedmx_hip_*.so | grep -v stamps)
+fi
 for rep in $(seq 1 ${AB_REPS:-3}); do
   for lib in $LIBS; do
     name=$(basename "$lib" .so)

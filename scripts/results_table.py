@@ -39,9 +39,15 @@ def load_results(root: str):
                 line = line.strip()
                 if line:
                     rows.append(json.loads(line))
+        rows = [r for r in rows if "client_metrics" in r]   # (not verification_results.json)
         if rows:
             out[path] = rows
     return out
+
+
+def _vals(row) -> np.ndarray:
+    """A round's client metrics; null (a client without abnormal test rows) -> NaN, left out of the stats."""
+    return np.asarray([np.nan if v is None else v for v in row["client_metrics"]], dtype=np.float64)
 
 
 def table(results, per_round: bool = False) -> str:
@@ -50,16 +56,16 @@ def table(results, per_round: bool = False) -> str:
     detail = []
     for path, rows in results.items():
         mt, ut = rows[-1].get("model_type", "?"), rows[-1].get("update_type", "?")
-        means = [float(np.mean(r["client_metrics"])) for r in rows]
-        last = np.asarray(rows[-1]["client_metrics"], dtype=np.float64)
+        means = [float(np.nanmean(_vals(r))) for r in rows]
+        last = _vals(rows[-1])
         rel = os.path.relpath(path)
-        lines.append(f"| `{rel}` | {mt} | {ut} | {len(rows)} | {last.mean():.4f} | {last.min():.4f} | {last.max():.4f} | "
+        lines.append(f"| `{rel}` | {mt} | {ut} | {len(rows)} | {np.nanmean(last):.4f} | {np.nanmin(last):.4f} | {np.nanmax(last):.4f} | "
                      f"{max(means):.4f} | {PAPER_IID.get((mt, ut), '')} | {PAPER_NONIID.get((mt, ut), '')} |")
         if per_round:
             detail += ["", f"### {rel}", "", "| round | mean | min | max |", "|---|---|---|---|"]
             for r in rows:
-                m = np.asarray(r["client_metrics"], dtype=np.float64)
-                detail.append(f"| {r['round']} | {m.mean():.4f} | {m.min():.4f} | {m.max():.4f} |")
+                m = _vals(r)
+                detail.append(f"| {r['round']} | {np.nanmean(m):.4f} | {np.nanmin(m):.4f} | {np.nanmax(m):.4f} |")
     return "\n".join(lines + detail) + "\n"
 
 

@@ -1,27 +1,29 @@
 """Long-horizon numerical parity of the fused training kernel at the paper's
-hyper-parameters (VERDICT r3 Next #3).
+hyper-parameters (VERDICT r3 Next #3, r4 Next #3).
 
 The paper configuration is 100 local epochs at lr 1e-5 and shrink lambda 10
 (`/root/reference/README.md:30-34`); the reference's local loop
 (`/root/reference/src/Trainer/client_trainer.py:360-419`) then runs ~5,700
 Adam steps per client-round on N-BaIoT-sized clients (~680 training rows,
-batch 12).  The short GPU tests stop at 3 epochs; this one runs the whole
-horizon in ONE launch of the helper-wave kernel (``fedmx_train_hw.hip``) and
-compares it with the plain-PyTorch oracle (``TorchEngine``: nn-free torch
-ops with the reference's op order, itself tested against ``nn.Module`` +
+batch 12; ~1,100 at the thesis's batch 64).  This test runs the whole horizon
+in ONE launch of the helper-wave kernel (``fedmx_train_hw.hip``; batch 64 is
+its MULTI instantiation: four 16-row chunks per Adam step) and compares it
+with the plain-PyTorch oracle (``TorchEngine``: nn-free torch ops with the
+reference's op order, itself tested against ``nn.Module`` +
 ``torch.optim.Adam``), patience disabled so every epoch runs.
 
-Agreement required: identical epochs run and best epoch, per-epoch train /
-validation losses within 1e-4 relative, final parameters within rtol 1e-3
-(atol 1e-5), Adam moments within rtol 1e-3 (atol 1e-6 / 1e-9).  The kernel's default Adam uses the
-hardware square root / reciprocal (<= 1 ulp each); the IEEE build
-(``-DFEDMX_EXACT_ADAM=1``, torch's rounding sequence with IEEE square root /
-division) is exercised by ``test_exact_adam_build_matches_torch_oracle`` in a
-child process that loads that library variant; it does NOT end closer to the
-oracle: client 1's trajectory at these hyper-parameters is sensitive to the
-last bit of the update (the two builds end 3.9e-5 apart in its parameters,
-each deterministic run to run), and the default build happens to track the
-oracle more closely (3e-8).
+Tolerances are the oracle's OWN sensitivity, not fitted numbers.  Client 1 of
+this data set is chaotic at these hyper-parameters: its latent codes shrink
+to ||z|| ~ 2e-5 on some rows (lambda 10), where the shrink penalty's gradient
+lambda z / (B ||z||) keeps unit size but takes its direction from z itself,
+i.e. from last-bit noise.  Re-running the oracle from initial parameters
+perturbed by 1 ulp moves client 1 by ~6.7e-5 in its final parameters and
+~1.5e-4 in its losses, client 0 by ~1e-7 (profiles/r5_long_horizon_sensitivity.md).
+So every comparison allows, per client and quantity, ``SENS_FACTOR`` times
+that measured 1-ulp divergence of the oracle, with the fixed floors below for
+the stable client: agreement to within the spread any two correct fp32
+implementations show.  Identical epochs run / best epoch / Adam step counts
+are required exactly.
 """
 import json
 import os
@@ -36,6 +38,13 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
+# floors: per-epoch losses 1e-4 relative; parameters / best snapshot rtol 1e-3
+# atol 1e-5; Adam moments rtol 1e-3 atol 1e-6 / 1e-9 (a first moment of a
+# near-zero gradient entry is itself tiny)
+LOSS_RTOL = 1e-4
+TOL = (("params", 1e-3, 1e-5), ("best", 1e-3, 1e-5), ("adam_m", 1e-3, 1e-6), ("adam_v", 1e-3, 1e-9))
+SENS_FACTOR = 3.0
+
 
 def _clients(seed=3):
     from fedmse_decentralized_amd.data.prepare import prepare_federation
@@ -46,111 +55,133 @@ def _clients(seed=3):
     return clients
 
 
-def _engines(clients, dev):
+def _init():
+    from fedmse_decentralized_amd.models.reference import init_client_params
+
+    return init_client_params(2, 0)[0]
+
+
+def _engines(clients, dev, init=None):
     from fedmse_decentralized_amd.engine.hip_engine import HipEngine
     from fedmse_decentralized_amd.engine.torch_engine import TorchEngine
     from fedmse_decentralized_amd.models.layout import DEFAULT_DIMS
-    from fedmse_decentralized_amd.models.reference import init_client_params
 
-    init, _ = init_client_params(2, 0)
+    init = _init() if init is None else init
     args = ([c.train for c in clients], [c.valid for c in clients], [c.test for c in clients],
             [c.test_label for c in clients], init)
     ref = TorchEngine(DEFAULT_DIMS, torch.device("cpu"))
     ref.setup(*args)
-    hip = HipEngine(DEFAULT_DIMS, dev)
-    hip.setup(*args)
+    hip = None
+    if dev is not None:
+        hip = HipEngine(DEFAULT_DIMS, dev)
+        hip.setup(*args)
     return ref, hip
 
 
-# (Adam's first moment of a near-zero gradient entry is itself tiny: 3 of
-# 18,432 entries differed by ~3e-7 absolute after 5,700 steps, so its
-# absolute floor is 1e-6; the parameters are held to rtol 1e-3 / atol 1e-5)
-TOL = (("params", 1e-3, 1e-5), ("best", 1e-3, 1e-5), ("adam_m", 1e-3, 1e-6), ("adam_v", 1e-3, 1e-9))
+def _set_anchor(engines, mu):
+    if not mu:
+        return
+    from fedmse_decentralized_amd.models.layout import canonical_to_padded, padded_to_canonical
+
+    base = engines[0].store.params.cpu()
+    anchor = base + 0.01 * torch.randn(base.shape, generator=torch.Generator().manual_seed(5))
+    anchor = canonical_to_padded(padded_to_canonical(anchor))
+    for e in engines:
+        e.store.anchor.copy_(anchor.to(e.store.anchor.device))
 
 
-def _compare(r1, r2, ref, hip, report=None):
+def sensitivity(clients, hp, r_ref, ref, seeds=(1, 2, 3)):
+    """The oracle against itself from 1-ulp-perturbed initial parameters:
+    per client, the max relative per-epoch loss difference and the max
+    absolute difference of every compared tensor, maximised over a few
+    random perturbations (a single one may happen not to set off a chaotic
+    trajectory's divergence: measured on the GPU box, one seed moved client 1
+    by 6e-6 where another moves it by 1.6e-4)."""
+    init = _init()
+    out = {c: {"loss_rel": 0.0, **{name: 0.0 for name, _, _ in TOL}} for c in range(2)}
+    for seed in seeds:
+        sign = torch.randint(0, 2, init.shape, generator=torch.Generator().manual_seed(seed)) * 2 - 1
+        pert = init * (1 + sign * 2.0 ** -23)
+        p, _ = _engines(clients, None, pert)
+        _set_anchor([p], hp.fedprox_mu)
+        r_p = p.train([0, 1], hp)
+        for c in range(2):
+            a, b = np.array(r_ref.tracking[c]), np.array(r_p.tracking[c])
+            d = out[c]
+            d["loss_rel"] = max(d["loss_rel"], float(np.max(np.abs(a - b) / np.abs(a))))
+            for name, _, _ in TOL:
+                d[name] = max(d[name], float((getattr(ref.store, name)[c] - getattr(p.store, name)[c]).abs().max()))
+    return out
+
+
+def _compare(r1, r2, ref, hip, sens, report=None):
+    """Kernel (r2, hip) against the oracle (r1, ref): exact epochs / best
+    epoch / step counts; losses and tensors within max(floor, SENS_FACTOR x
+    the oracle's own 1-ulp sensitivity) per client."""
     stats = {"epochs_run": [list(map(int, r1.epochs_run)), list(map(int, r2.epochs_run))],
-             "best_epoch": [list(map(int, r1.best_epoch)), list(map(int, r2.best_epoch))]}
-    for i, (a, b) in enumerate(zip(r1.tracking, r2.tracking)):
-        a, b = np.array(a), np.array(b)
-        stats[f"loss_rel_max_c{i}"] = float(np.max(np.abs(b - a) / np.abs(a)))
-    for name, _, _ in TOL:
-        x, y = getattr(hip.store, name).cpu().double(), getattr(ref.store, name).double()
-        stats[f"{name}_abs_max"] = float((x - y).abs().max())
-        stats[f"{name}_rel_max"] = float(((x - y).abs() / y.abs().clamp_min(1e-30)).max())
+             "best_epoch": [list(map(int, r1.best_epoch)), list(map(int, r2.best_epoch))], "sensitivity": sens}
+    bad = []
+    for c in range(2):
+        a, b = np.array(r1.tracking[c]), np.array(r2.tracking[c])
+        rel = float(np.max(np.abs(b - a) / np.abs(a)))
+        lim = max(LOSS_RTOL, SENS_FACTOR * sens[c]["loss_rel"])
+        stats[f"loss_rel_max_c{c}"] = rel
+        if rel > lim:
+            bad.append(f"client {c} losses rel {rel:.3g} > {lim:.3g}")
+        for name, rtol, atol in TOL:
+            x = getattr(hip.store, name)[c].cpu().double()
+            y = getattr(ref.store, name)[c].double()
+            d = (x - y).abs()
+            stats[f"{name}_abs_max_c{c}"] = float(d.max())
+            lim_abs = max(atol, SENS_FACTOR * sens[c][name])
+            over = d > (lim_abs + rtol * y.abs())
+            if bool(over.any()):
+                bad.append(f"client {c} {name}: {int(over.sum())} entries beyond atol {lim_abs:.3g} + rtol {rtol} "
+                           f"(max abs diff {float(d.max()):.3g})")
     print("long-horizon stats", json.dumps(stats), flush=True)   # on record even when an assertion fails
     if report is not None:
         report.update(stats)
     assert list(r1.epochs_run) == list(r2.epochs_run)
     assert list(r1.best_epoch) == list(r2.best_epoch)
-    for a, b in zip(r1.tracking, r2.tracking):
-        np.testing.assert_allclose(np.array(b), np.array(a), rtol=1e-4, atol=0)
-    for name, rtol, atol in TOL:
-        torch.testing.assert_close(getattr(hip.store, name).cpu().double(), getattr(ref.store, name).double(),
-                                   rtol=rtol, atol=atol)
     assert torch.equal(hip.store.adam_step.cpu(), ref.store.adam_step)
+    assert not bad, bad
     return stats
 
 
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("mu", [0.0, 0.001], ids=["fedmse-sae", "fedprox"])
-def test_paper_config_100_epochs_matches_torch_oracle(mu):
+def _run_case(dev, mu, batch):
     from fedmse_decentralized_amd.engine.base import TrainHParams
 
-    dev = torch.device("cuda", 0)
-    ref, hip = _engines(_clients(), dev)
-    if mu:
-        anchor = ref.store.params + 0.01 * torch.randn(ref.store.params.shape,
-                                                       generator=torch.Generator().manual_seed(5))
-        from fedmse_decentralized_amd.models.layout import canonical_to_padded, padded_to_canonical
-
-        anchor = canonical_to_padded(padded_to_canonical(anchor))
-        ref.store.anchor.copy_(anchor)
-        hip.store.anchor.copy_(anchor.to(dev))
-    hp = TrainHParams(epochs=100, batch_size=12, lr=1e-5, shrink_lambda=10.0, fedprox_mu=mu, patience=10 ** 6)
+    clients = _clients()
+    ref, hip = _engines(clients, dev)
+    _set_anchor([ref, hip], mu)
+    hp = TrainHParams(epochs=100, batch_size=batch, lr=1e-5, shrink_lambda=10.0, fedprox_mu=mu, patience=10 ** 6)
     r1 = ref.train([0, 1], hp)
     r2 = hip.train([0, 1], hp)
     assert list(r2.epochs_run) == [100, 100]
-    assert int(hip.store.adam_step[0]) == 100 * ((ref.store.train_off[1] - ref.store.train_off[0] + 11) // 12)
-    stats = _compare(r1, r2, ref, hip)
-    print("long-horizon", json.dumps(stats))
+    n0 = int(ref.store.train_off[1] - ref.store.train_off[0])
+    assert int(hip.store.adam_step[0]) == 100 * ((n0 + batch - 1) // batch)
+    sens = sensitivity(clients, hp, r1, ref)
+    return _compare(r1, r2, ref, hip, sens)
 
 
-def _compare_exact(r1, r2, ref, hip, report):
-    """The IEEE-Adam build: client 0 to the default build's tolerances; client 1,
-    whose trajectory is the sensitive one at these hyper-parameters (the
-    IEEE and the default builds themselves end 3.9e-5 apart in its
-    parameters, each run deterministic: profiles/r4_train_hw_experiments.md),
-    to 5e-4 in the losses and 2e-4 absolute in the parameters."""
-    assert list(r1.epochs_run) == list(r2.epochs_run)
-    assert list(r1.best_epoch) == list(r2.best_epoch)
-    loss_tol = (1e-4, 5e-4)
-    par_atol = (1e-5, 2e-4)
-    for c in range(2):
-        a, b = np.array(r1.tracking[c]), np.array(r2.tracking[c])
-        rel = float(np.max(np.abs(b - a) / np.abs(a)))
-        x = hip.store.params[c].cpu().double()
-        y = ref.store.params[c].double()
-        d = float((x - y).abs().max())
-        report[f"c{c}"] = {"loss_rel_max": rel, "params_abs_max": d}
-        assert rel <= loss_tol[c], (c, rel)
-        assert d <= par_atol[c], (c, d)
-    assert torch.equal(hip.store.adam_step.cpu(), ref.store.adam_step)
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("batch", [12, 64], ids=["b12", "b64"])
+@pytest.mark.parametrize("mu", [0.0, 0.001], ids=["fedmse-sae", "fedprox"])
+def test_paper_config_100_epochs_matches_torch_oracle(mu, batch):
+    """Batch 12 (the code default, compact one-chunk step) and batch 64 (the
+    thesis's GPU runs, SURVEY §5.6: the MULTI instantiation, four 16-row
+    chunks per Adam step with the weight gradients accumulated over them)."""
+    stats = _run_case(torch.device("cuda", 0), mu, batch)
+    print("long-horizon", f"mu={mu} batch={batch}", json.dumps(stats))
 
 
 _CHILD = r"""
 import json, sys, torch
 sys.path.insert(0, sys.argv[1])
 sys.path.insert(0, sys.argv[1] + "/tests")
-from test_long_horizon_gpu import _clients, _engines, _compare_exact
-from fedmse_decentralized_amd.engine.base import TrainHParams
+from test_long_horizon_gpu import _run_case
 from fedmse_decentralized_amd.ops import _hip
-ref, hip = _engines(_clients(), torch.device("cuda", 0))
-hp = TrainHParams(epochs=100, batch_size=12, lr=1e-5, shrink_lambda=10.0, patience=10 ** 6)
-r1 = ref.train([0, 1], hp)
-r2 = hip.train([0, 1], hp)
-st = {}
-_compare_exact(r1, r2, ref, hip, st)
+st = _run_case(torch.device("cuda", 0), 0.0, 12)
 st["lib"] = _hip.lib_path()
 print(json.dumps(st))
 """
@@ -158,14 +189,15 @@ print(json.dumps(st))
 
 @pytest.mark.timeout(600)
 def test_exact_adam_build_matches_torch_oracle():
-    """The IEEE-division Adam build (-DFEDMX_EXACT_ADAM=1, built by
-    ``__graft_entry__.build()`` as ``libfedmx_hip_exact.so``) over the same
-    100-epoch horizon, in a child process that loads that library
-    (tolerances: ``_compare_exact``)."""
+    """The IEEE-division Adam build (-DFEDMX_EXACT_ADAM=1: torch's rounding
+    sequence, unscaled moments; ``libfedmx_hip_exact.so``) over the same
+    horizon, in a child process that loads that library, to the same
+    sensitivity-derived tolerances as the default build."""
     from fedmse_decentralized_amd.ops import build
 
-    lib = build.HIP_EXACT_LIB
-    assert lib.exists(), f"{lib} missing: run __graft_entry__.build()"
+    # rebuilt here when its content hash (sources, flags, compiler) is stale,
+    # so an edited kernel source is never tested through an old library
+    lib = build.build_hip(extra_flags=["-DFEDMX_EXACT_ADAM=1"], target=build.HIP_EXACT_LIB)
     env = dict(os.environ, FEDMX_HIP_LIB=str(lib))
     r = subprocess.run([sys.executable, "-c", _CHILD, ROOT], env=env, capture_output=True, text=True, timeout=500)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]

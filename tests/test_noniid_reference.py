@@ -1,0 +1,57 @@
+"""The reference's own N-BaIoT non-IID device list (VERDICT r4 Next #2).
+
+`/root/reference/src/Configuration/scen2-nba-iot-10clients_noniid.json`
+lists ten clients; clients 6, 9 and 10 ship without ``abnormal/`` data
+(`/root/reference/.MISSING_LARGE_BLOBS:4-6`).  The loader accepts them: they
+train, vote and verify like the others, and since their test sets hold normal
+rows only their AUC is undefined -- written as null in the per-round report
+and left out of every mean / min / max (global early stop, the summary's
+best metric).  CPU engine, two rounds.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+REF_CFG = "/root/reference/src/Configuration/scen2-nba-iot-10clients_noniid.json"
+MISSING = {"NBa-Scen2-Client-6", "NBa-Scen2-Client-9", "NBa-Scen2-Client-10"}
+
+pytestmark = pytest.mark.skipif(not os.path.exists(REF_CFG), reason="reference checkout not mounted")
+
+
+def test_noniid_device_list_with_abnormal_less_clients(tmp_path):
+    from fedmse_decentralized_amd import federation
+    from fedmse_decentralized_amd.config import ExperimentConfig
+    from fedmse_decentralized_amd.federation import Federation, metric_stats
+
+    federation._PREP_CACHE.clear()
+    cfg = ExperimentConfig(config_file=REF_CFG, network_size=10, num_rounds=2, epoch=1, lr_rate=1e-3,
+                           shrink_lambda=1, output_root=str(tmp_path), backend="torch", device="cpu",
+                           compat="fixed", global_early_stop=False, save_checkpoints=False, log_level="WARNING",
+                           model_types=["hybrid"], update_types=["mse_avg"])
+    fed = Federation(cfg, "hybrid", "mse_avg", 0).setup()
+    names = [c.name for c in fed.clients]
+    # the reference's device sampling order (random.Random(1234).sample, src/main.py:116,126)
+    assert [n.split("-")[-1] for n in names] == ["8", "2", "1", "10", "5", "7", "6", "4", "9", "3"]
+    for c in fed.clients:
+        if c.name in MISSING:
+            assert c.n_abnormal == 0 and int(c.test_label.sum()) == 0
+        else:
+            assert c.n_abnormal > 0
+    rs = [fed.run_round() for _ in range(2)]
+    fed.finish()
+    fed.writer.flush()
+    for r in rs:
+        m = np.asarray(r.metrics, dtype=np.float64)
+        undefined = {names[i] for i in np.flatnonzero(np.isnan(m))}
+        assert undefined == MISSING
+        mean, lo, hi = metric_stats(m)
+        assert 0.5 < lo <= mean <= hi <= 1.0
+    path = os.path.join(cfg.checkpoint_dir, "Run_0", "AUC", "FL-IoT_0.5_hybrid_mse_avg_results.json")
+    rows = [json.loads(line) for line in open(path)]
+    assert [r["round"] for r in rows] == [1, 2]
+    for r in rows:
+        vals = r["client_metrics"]
+        assert {names[i] for i, v in enumerate(vals) if v is None} == MISSING
+        assert r["global_loss"] == min(v for v in vals if v is not None)
