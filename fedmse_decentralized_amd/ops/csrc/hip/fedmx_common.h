@@ -52,6 +52,16 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
+// ReLU as ONE integer v_max_i32 on the float's bits: a negative float (sign
+// bit set) is a negative int, so max(bits, 0) is +0.0 for it (and for -0.0)
+// and the float itself otherwise -- max(x, 0) for every non-NaN x.
+// fmaxf(x, 0.f) (or an fmed3 with 0 and +inf, which the compiler folds into
+// it) on an MFMA result costs two VALU instructions: the compiler cannot
+// prove the accumulator canonical and quiets it first (v_max_f32 x, x).
+__device__ __forceinline__ float relu(float x) {
+  return __builtin_bit_cast(float, max(__builtin_bit_cast(int, x), 0));
+}
+
 __device__ __forceinline__ f32x4 lds_read4(const float* p) {
   return *reinterpret_cast<const f32x4*>(p);
 }

@@ -198,7 +198,7 @@ __device__ __forceinline__ void fwd_rows_block(const FwdDesc& d, const float* sW
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = fmaxf(acc[r], 0.0f);
+        float v = relu(acc[r]);
         if (16 * t + 4 * g + r == H_BIAS) v = 1.0f;
         acc[r] = v;
       }
@@ -236,7 +236,7 @@ __device__ __forceinline__ void fwd_rows_block(const FwdDesc& d, const float* sW
       for (int s = 0; s < (CP ? 2 : 4); ++s) acc = mfma16(a[s], z[s], acc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = fmaxf(acc[r], 0.0f);
+        float v = relu(acc[r]);
         if (16 * t + 4 * g + r == H_BIAS) v = 1.0f;
         acc[r] = v;
       }

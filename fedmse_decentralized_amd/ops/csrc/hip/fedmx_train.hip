@@ -421,7 +421,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float vv = fmaxf(s[r], 0.f);
+        float vv = relu(s[r]);
         if (hbias_d[t][r]) vv = 1.f;
         s[r] = vv;
       }
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v0 = fmaxf(acc0[r], 0.f), v1 = fmaxf(acc1[r], 0.f);
+        float v0 = relu(acc0[r]), v1 = relu(acc1[r]);
         if (hbias_d[0][r]) v0 = 1.f;
         if (hbias_d[1][r]) v1 = 1.f;
         acc0[r] = v0;
@@ -543,7 +543,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v0 = fmaxf(sum0[r], 0.f), v1 = fmaxf(sum1[r], 0.f);
+        float v0 = relu(sum0[r]), v1 = relu(sum1[r]);
         if (hbias_d[0][r]) v0 = 1.f;
         if (hbias_d[1][r]) v1 = 1.f;
         sum0[r] = v0;
@@ -569,7 +569,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v0 = fmaxf(acc0[r], 0.f), v1 = fmaxf(acc1[r], 0.f);
+        float v0 = relu(acc0[r]), v1 = relu(acc1[r]);
         if (hbias_d[0][r]) v0 = 1.f;
         if (hbias_d[1][r]) v1 = 1.f;
         acc0[r] = v0;

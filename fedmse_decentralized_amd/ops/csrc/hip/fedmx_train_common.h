@@ -422,7 +422,9 @@ __device__ __forceinline__ void global_to_masters_o(const float* __restrict__ sr
   }
 }
 
-template <bool CP>
+// CLEAR_BU: the helper-wave kernel's in-launch bias units (the last element
+// of W1, W2 and W3, fedmx_train_hw.hip FEDMX_HW_BIAS_UNITS) are written as 0
+template <bool CP, bool CLEAR_BU = false>
 __device__ __forceinline__ void masters_to_global_o(float* __restrict__ dst, float* sW1, float* sW4, float* sW2,
                                                     float* sW3) {
   f32x4* d4 = reinterpret_cast<f32x4*>(dst);
@@ -436,6 +438,8 @@ __device__ __forceinline__ void masters_to_global_o(float* __restrict__ dst, flo
 #pragma unroll
       for (int i = 0; i < 4; ++i) val[k][i] = *master_slot<CP>(e, i, sW1, sW4, sW2, sW3);
     }
+    if (CLEAR_BU && (e == OFF_W1 + HP * DP - 4 || e == OFF_W2 + ZP * HP - 4 || e == OFF_W3 + HP * ZP - 4))
+      val[k][3] = 0.f;
   }
 #pragma unroll
   for (int k = 0; k < STAGE_PER_THREAD; ++k) d4[threadIdx.x + 256 * k] = val[k];

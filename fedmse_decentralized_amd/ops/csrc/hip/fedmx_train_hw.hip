@@ -69,6 +69,27 @@
 #ifndef FEDMX_HW_FLAGS
 #define FEDMX_HW_FLAGS 0
 #endif
+// 1: the constant-1 "bias units" of H1, Z and H3 (the slots that feed b2, b3
+// and b4 through the next layer's bias column) come out of the products
+// themselves instead of being set by a select after every product: inside
+// the launch W1's bias row, W2's bias row and W3's bias row hold a single 1
+// (in the input-bias column, the H1-bias column and the Z-bias column), so
+// relu(1 * 1) = 1, 1 * 1 = 1 and relu(1 * 1) = 1 exactly.  Their gradients
+// are zero (the dH1 / dZ / dH3 masks already exclude the bias slots), so Adam
+// never moves them; the global parameters (aggregation, checkpoints) never
+// see them: set on staging in, cleared on staging out (bias_units_*).
+#ifndef FEDMX_HW_BIAS_UNITS
+#define FEDMX_HW_BIAS_UNITS 1
+#endif
+// 1: the backward masks test values, not slot tables: every padded hidden /
+// latent slot holds exactly 0 (zero weights, relu(0) = 0, zero gradients),
+// so "real and positive" is "positive" except at the one bias slot, which a
+// per-lane threshold (2 > the bias unit's 1) or a single-slot select
+// excludes: one compare + select per element instead of compare + scalar AND
+// + select, and no select at all on the latent axis but the bias slot's
+#ifndef FEDMX_HW_VALUE_MASKS
+#define FEDMX_HW_VALUE_MASKS 1
+#endif
 // the same switch for the FedProx instantiation: 1 there (r4 A/B: FedProx
 // launch -3.3 %, the plain launch +6 % -- without FedProx the helpers' path is
 // short enough that the flag polls only add latency to the mains')
@@ -139,6 +160,20 @@ struct MSlab {
 struct HSlab {
   float q4[2][2][4];
 };
+
+// storage-order float4 index of each bias-unit entry (the last element of
+// W1 [HP][DP], W2 [ZP][HP], W3 [HP][ZP]: their bias row, bias column)
+constexpr int BU_W1 = (OFF_W1 + HP * DP - 4) / 4;
+constexpr int BU_W2 = (OFF_W2 + ZP * HP - 4) / 4;
+constexpr int BU_W3 = (OFF_W3 + HP * ZP - 4) / 4;
+// staging thread's share (stage_load layout): mark / clear the bias units
+__device__ __forceinline__ void bias_units_set(f32x4 (&val)[STAGE_PER_THREAD], float one) {
+#pragma unroll
+  for (int k = 0; k < STAGE_PER_THREAD; ++k) {
+    const int q = threadIdx.x + 256 * k;
+    if (q == BU_W1 || q == BU_W2 || q == BU_W3) val[k][3] = one;
+  }
+}
 
 struct Lane {
   float* w1;   // sW1 + c*S_W1 + 32w + 4g
@@ -295,6 +330,10 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   const float* const d3p = sW3 + 4 * g * S_W3 + c;
   const int tw = 4 * g * S_T + c;
   const int tr = c * S_T + 4 * g;
+  // owned small tile's operands (wave-uniform choice, made once): w < 2: dW3
+  // tile = dH3^T(rows 16w..) Z; w >= 2: dW2 tile = dZ^T H1(tile w-2)
+  const float* const sm_a = w < 2 ? sT2 + tr + 16 * w * S_T : sDZT + tr;
+  const float* const sm_b = w < 2 ? sZT + tr : sH1T + tr + 16 * (w - 2) * S_T;
   float* const redw = sRedDH3 + (w * 2) * 256 + lane * 4;
 
   const int kslot = blockIdx.x;
@@ -339,6 +378,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     zreal_d[r] = j < latent;
     zbias_d[r] = j == z_bias_slot<CP>();
   }
+  // FEDMX_HW_VALUE_MASKS: the bias slots in the register tiles (compact
+  // order): H3 / dH3 D-layout row 30 = tile 1, (g, r) = (3, 2); H1^T row 30 =
+  // tile 1, column lane c = 14; Z D-layout row 13 = (g, r) = (3, 1)
+  const float thr_h3b = (g == 3) ? 2.f : 0.f;
+  const float thr_h1b = (c == 14) ? 2.f : 0.f;
+  const bool z_bias_lane = (g == 3);
   const int brow_c = batch_row_of_col<CPB>(c);
   int brow_b[4];
 #pragma unroll
@@ -435,9 +480,9 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v0 = fmaxf(sum0[r], 0.f), v1 = fmaxf(sum1[r], 0.f);
-        if (hbias_d[0][r]) v0 = 1.f;
-        if (hbias_d[1][r]) v1 = 1.f;
+        float v0 = relu(sum0[r]), v1 = relu(sum1[r]);
+        if (!FEDMX_HW_BIAS_UNITS && hbias_d[0][r]) v0 = 1.f;
+        if (!FEDMX_HW_BIAS_UNITS && hbias_d[1][r]) v1 = 1.f;
         sum0[r] = v0;
         sum1[r] = v1;
       }
@@ -448,7 +493,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     f32x4 zb = z;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (zbias_d[r]) zb[r] = 1.f;
+      if (!FEDMX_HW_BIAS_UNITS && zbias_d[r]) zb[r] = 1.f;
     f32x4 h3[2];
     {
       f32x4 acc0 = zero4(), acc1 = zero4();
@@ -461,9 +506,9 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v0 = fmaxf(acc0[r], 0.f), v1 = fmaxf(acc1[r], 0.f);
-        if (hbias_d[0][r]) v0 = 1.f;
-        if (hbias_d[1][r]) v1 = 1.f;
+        float v0 = relu(acc0[r]), v1 = relu(acc1[r]);
+        if (!FEDMX_HW_BIAS_UNITS && hbias_d[0][r]) v0 = 1.f;
+        if (!FEDMX_HW_BIAS_UNITS && hbias_d[1][r]) v1 = 1.f;
         acc0[r] = v0;
         acc1[r] = v1;
       }
@@ -471,8 +516,13 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       h3[1] = acc1;
     }
     float nz = 0.f;
+    if (FEDMX_HW_VALUE_MASKS) {
+      // (padded latent slots are 0; the bias slot is row (g, r) = (3, 1))
+      nz = z[0] * z[0] + (z_bias_lane ? 0.f : z[1] * z[1]) + z[2] * z[2] + z[3] * z[3];
+    } else {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) nz += zreal_d[r] ? z[r] * z[r] : 0.f;
+      for (int r = 0; r < 4; ++r) nz += zreal_d[r] ? z[r] * z[r] : 0.f;
+    }
     nz = sum_lane_groups(nz);
     const float norm_v = __builtin_amdgcn_sqrtf(nz);
 #pragma unroll
@@ -584,7 +634,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       min_valid = valid_loss;
       best_ep = ep;
       worse = 0;
-      if (stager) masters_to_global_o<CP>(Bg, sW1, sW4, sW2, sW3);  // save_model(): best snapshot
+      if (stager) masters_to_global_o<CP, FEDMX_HW_BIAS_UNITS>(Bg, sW1, sW4, sW2, sW3);  // save_model(): best snapshot
     } else {
       ++worse;
     }
@@ -603,6 +653,10 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     stage_load(Vg, pv_v);
     if (PROX) stage_load(A.anchor + (size_t)cid * P_PAD, pv_a);
     stage_load(Pg, pv_p);
+    if (FEDMX_HW_BIAS_UNITS) {
+      bias_units_set(pv_p, 1.f);
+      if (PROX) bias_units_set(pv_a, 1.f);   // (p - anchor = 0 there: no proximal pull)
+    }
   }
   auto stage_vals = [&](const f32x4 (&v)[STAGE_PER_THREAD]) {
     if (stager) vals_to_masters_o<CP>(v, sW1, sW4, sW2, sW3);
@@ -918,8 +972,8 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float vv = fmaxf(s[r], 0.f);
-            if (hbias_d[t][r]) vv = 1.f;
+            float vv = relu(s[r]);
+            if (!FEDMX_HW_BIAS_UNITS && hbias_d[t][r]) vv = 1.f;
             s[r] = vv;
           }
           h1[t] = s;
@@ -929,7 +983,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         zb = z;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (zbias_d[r]) zb[r] = 1.f;
+          if (!FEDMX_HW_BIAS_UNITS && zbias_d[r]) zb[r] = 1.f;
         {
           f32x4 acc0 = zero4(), acc1 = zero4();
           const f32x4 a0 = lds_read4(a3p);
@@ -941,9 +995,9 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float v0 = fmaxf(acc0[r], 0.f), v1 = fmaxf(acc1[r], 0.f);
-            if (hbias_d[0][r]) v0 = 1.f;
-            if (hbias_d[1][r]) v1 = 1.f;
+            float v0 = relu(acc0[r]), v1 = relu(acc1[r]);
+            if (!FEDMX_HW_BIAS_UNITS && hbias_d[0][r]) v0 = 1.f;
+            if (!FEDMX_HW_BIAS_UNITS && hbias_d[1][r]) v1 = 1.f;
             acc0[r] = v0;
             acc1[r] = v1;
           }
@@ -984,8 +1038,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         const bool col_ok = (unsigned)brow_c < (unsigned)bc;
         sq = col_ok ? sq : 0.f;
         float nz = 0.f;
+        if (FEDMX_HW_VALUE_MASKS) {
+          nz = z[0] * z[0] + (z_bias_lane ? 0.f : z[1] * z[1]) + z[2] * z[2] + z[3] * z[3];
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) nz += zreal_d[r] ? z[r] * z[r] : 0.f;
+          for (int r = 0; r < 4; ++r) nz += zreal_d[r] ? z[r] * z[r] : 0.f;
+        }
         nz = sum_lane_groups(nz);
         norm_c = __builtin_amdgcn_sqrtf(nz);
         float contrib = sq * (inv_bt * inv_d);
@@ -1055,7 +1113,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           for (int r = 0; r < 4; ++r) s[r] = s[r] + o[r];
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s[r] = (hreal_d[t][r] && h3[t][r] > 0.f) ? s[r] : 0.f;
+        for (int r = 0; r < 4; ++r) {
+          if (FEDMX_HW_VALUE_MASKS)
+            s[r] = (h3[t][r] > ((t == 1 && r == 2) ? thr_h3b : 0.f)) ? s[r] : 0.f;
+          else
+            s[r] = (hreal_d[t][r] && h3[t][r] > 0.f) ? s[r] : 0.f;
+        }
         dh3[t] = s;
       }
       float prox_acc = 0.f;
@@ -1070,7 +1133,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       const float shr_raw = lam * __builtin_amdgcn_rcpf((float)bt * norm_c);
       const float shr = (col_ok && norm_c > 0.f) ? shr_raw : 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dz[r] = zreal_d[r] ? dz[r] + shr * z[r] : 0.f;
+      for (int r = 0; r < 4; ++r) {
+        if (FEDMX_HW_VALUE_MASKS)
+          dz[r] = (r == 1 && z_bias_lane) ? 0.f : dz[r] + shr * z[r];
+        else
+          dz[r] = zreal_d[r] ? dz[r] + shr * z[r] : 0.f;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) sDZT[tw + r * S_T] = dz[r];
       // ---- dH1 (batch-major) with the ReLU mask from H1^T
@@ -1083,7 +1151,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
         for (int s = 0; s < KZ; ++s) acc = mfma16(dz[s], q2[t][s], acc);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = (hreal_c[t] && h1b[t][r] > 0.f) ? acc[r] : 0.f;
+        for (int r = 0; r < 4; ++r) {
+          if (FEDMX_HW_VALUE_MASKS)
+            acc[r] = (h1b[t][r] > (t == 1 ? thr_h1b : 0.f)) ? acc[r] : 0.f;
+          else
+            acc[r] = (hreal_c[t] && h1b[t][r] > 0.f) ? acc[r] : 0.f;
+        }
         dh1b[t] = acc;
       }
       HSTAMP(ms, 8);
@@ -1098,9 +1171,8 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       wave_sync();
       // ---- owned small tile: w<2 -> dW3 tile = dH3^T Z ; w>=2 -> dW2 tile = dZ^T H1
       if (!(FEDMX_HW_ABLATE & 4)) {
-        const f32x4 a = lds_read4(w < 2 ? sT2 + tr + 16 * w * S_T : sDZT + tr);
-        const f32x4 bz = lds_read4(sZT + tr);
-        const f32x4 b = (w < 2) ? bz : ((w == 2) ? h1b[0] : h1b[1]);
+        const f32x4 a = lds_read4(sm_a);
+        const f32x4 b = lds_read4(sm_b);   // (Z^T, or H1^T's tile of this wave)
 #pragma unroll
         for (int s = 0; s < KB; ++s) Go = mfma16(a[s], b[s], Go);
       }
@@ -1175,7 +1247,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // ---- write back: params (masters), then m and v through the same staging
   HSTAMP(true, 30);
   __syncthreads();
-  masters_to_global_o<CP>(Pg, sW1, sW4, sW2, sW3);
+  masters_to_global_o<CP, FEDMX_HW_BIAS_UNITS>(Pg, sW1, sW4, sW2, sW3);
   if (FEDMX_HW_SCALED) {
     scale_mslab(M, K.one_m_b1);
     scale_mslab(V, K.one_m_b2);

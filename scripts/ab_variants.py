@@ -25,7 +25,8 @@ VARIANTS = {
     # r4: pipelined W1 Adam (pipe, flags_pipe, flags2_pipe), the SPLIT step (hwsplit,
     # hwsplitd1/2) and grouped dH3 reads (red8) measured slower and were removed from
     # the kernel (profiles/r4_train_hw_experiments.md; source in git history, commit ef22669)
-    "hwscaled0": ["-DFEDMX_HW_SCALED=0"],           # r5: unscaled FMA Adam in the helper-wave kernel (the r4 production step)
+    "hwscaled0": ["-DFEDMX_HW_SCALED=0"],           # r5: unscaled FMA Adam in the helper-wave kernel: 897 vs 870 us (-3.0 %)
+    "nobu": ["-DFEDMX_HW_BIAS_UNITS=0", "-DFEDMX_HW_VALUE_MASKS=0"],   # r5: bias slots by select, slot-table masks
     "exact": ["-DFEDMX_EXACT_ADAM=1"],               # r4: IEEE sqrt / division Adam (torch's op sequence)
     "flags": ["-DFEDMX_HW_FLAGS=1"],                 # r4: mains-only layer-1 exchange + helper->main LDS flags
     "flags_madam": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=32"],   # timing only: + mains skip W1 Adam

@@ -24,6 +24,11 @@ run() {
   echo "$name rc=$rc $(tail -n 1 "$OUT/$name.log" | cut -c1-200)"
   return $rc
 }
-run tableA_noniid && \
-run noniid_a005 --synthetic-alpha 0.05 && \
-run noniid_poison3 --malicious-clients 3 --malicious-scale 10
+# SETTINGS="tableA_noniid noniid_a005 noniid_poison3" (default: all three)
+for s in ${SETTINGS:-tableA_noniid noniid_a005 noniid_poison3}; do
+  case $s in
+    tableA_noniid) run tableA_noniid || exit $? ;;
+    noniid_a005) run noniid_a005 --synthetic-alpha 0.05 || exit $? ;;
+    noniid_poison3) run noniid_poison3 --malicious-clients 3 --malicious-scale 10 || exit $? ;;
+  esac
+done

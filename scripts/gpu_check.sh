@@ -12,7 +12,7 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 TESTS=${TESTS:-"tests/test_kernels_gpu.py tests/test_long_horizon_gpu.py"}
 if [ "$TESTS" != none ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest -x -v --timeout 600 --timeout-method thread $TESTS \
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${PYTEST_X--x} -v --timeout 600 --timeout-method thread $TESTS \
     > "$OUT/tests.log" 2>&1
   rc=$?
   tail -n 5 "$OUT/tests.log"

@@ -116,25 +116,32 @@ def test_hip_256_client_federation_does_not_collapse(tmp_path):
     assert min(means) > 0.96, means
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 def test_bench_config_20_rounds_matches_oracle(tmp_path):
     """VERDICT r3 Weak #4 (end-to-end horizon): the headline configuration
     (10 N-BaIoT-sized clients, 50 % participation, 5 local epochs, fixed
     compat, shared initial model) for 20 rounds, the HIP engine's
     device-resident round against the plain-PyTorch CPU engine's host round.
-    Every discrete outcome (selections, elected aggregator, each receiver's
-    verification decision) must agree in every round, and the per-client
-    AUCs stay within fp32-trajectory tolerance."""
+
+    The protocol's discrete outcomes are themselves sensitive at the last
+    bit: the oracle re-run with lr x (1 + 2^-23) elects a different
+    aggregator from round 5 on (profiles/r5_long_horizon_sensitivity.md: a
+    near-tie of two candidates' vote scores).  So the HIP run must agree with
+    the oracle in every discrete outcome (selection, aggregator, each
+    receiver's verification decision) for at least as many rounds as the
+    oracle agrees with that perturbed copy of itself, with per-client AUCs
+    within 5e-3 there; and over all 20 rounds its per-round mean AUC must stay
+    as close to the oracle's as the perturbed oracle's does (x2, floor 5e-3)."""
     from fedmse_decentralized_amd import federation
     from fedmse_decentralized_amd.federation import Federation
 
     rounds = 20
-    runs = {}
-    for backend, device in (("hip", "cuda"), ("torch", "cpu")):
+
+    def run(backend, device, lr):
         cfg = ExperimentConfig(synthetic="nbaiot", network_size=10, num_rounds=rounds, epoch=5, batch_size=12,
-                               output_root=str(tmp_path / backend), backend=backend, device=device,
-                               log_level="WARNING", compat="fixed", global_early_stop=False, save_checkpoints=False,
-                               model_types=["hybrid"], update_types=["mse_avg"])
+                               lr_rate=lr, output_root=str(tmp_path / f"{backend}{lr}"), backend=backend,
+                               device=device, log_level="ERROR", compat="fixed", global_early_stop=False,
+                               save_checkpoints=False, model_types=["hybrid"], update_types=["mse_avg"])
         federation._PREP_CACHE.clear()
         fed = Federation(cfg, "hybrid", "mse_avg", 0, write_reports=False).setup()
         assert (fed._fast is not None) == (backend == "hip")
@@ -144,12 +151,26 @@ def test_bench_config_20_rounds_matches_oracle(tmp_path):
             ver = [(v["client_id"], v["is_verified"]) for v in (r.verification or [])]
             out.append((r.selected, r.aggregator, ver, np.array(r.metrics)))
         fed.finish()
-        runs[backend] = out
-    worst = 0.0
-    for i, ((sh, ah, vh, mh), (st, at, vt, mt)) in enumerate(zip(runs["hip"], runs["torch"])):
-        assert sh == st, f"round {i + 1}: selection"
-        assert ah == at, f"round {i + 1}: aggregator"
-        assert vh == vt, f"round {i + 1}: verification"
-        worst = max(worst, float(np.abs(mh - mt).max()))
-    print(f"bench config, {rounds} rounds: max |AUC hip - oracle| = {worst:.2e}")
+        return out
+
+    hip = run("hip", "cuda", 1e-3)
+    ref = run("torch", "cpu", 1e-3)
+    pert = run("torch", "cpu", 1e-3 * (1 + 2.0 ** -23))
+
+    def horizon(a, b):
+        for i, (x, y) in enumerate(zip(a, b)):
+            if x[:3] != y[:3]:
+                return i
+        return rounds
+
+    h_oracle = horizon(ref, pert)
+    h_hip = horizon(hip, ref)
+    worst = max((float(np.abs(hip[i][3] - ref[i][3]).max()) for i in range(h_hip)), default=0.0)
+    mean_gap = max(abs(float(hip[i][3].mean() - ref[i][3].mean())) for i in range(rounds))
+    mean_gap_oracle = max(abs(float(pert[i][3].mean() - ref[i][3].mean())) for i in range(rounds))
+    print(f"bench config, {rounds} rounds: discrete agreement hip/oracle {h_hip} rounds, oracle/perturbed oracle "
+          f"{h_oracle}; max |AUC hip - oracle| while agreeing {worst:.2e}; max per-round mean-AUC gap hip "
+          f"{mean_gap:.2e}, perturbed oracle {mean_gap_oracle:.2e}")
+    assert h_hip >= min(h_oracle, rounds), (h_hip, h_oracle)
     assert worst < 5e-3
+    assert mean_gap <= max(5e-3, 2 * mean_gap_oracle)
