@@ -142,10 +142,10 @@ def main(argv=None):
     if _probe_wanted(known):
         # before this process touches the GPU: the first transport that works
         # on every rank (RCCL, else peer-memory IPC, else gloo)
-        requested = known.comm or os.environ.get("FEDMX_COMM") or "rccl"
+        requested = probe.requested_transport(known.comm)
         used, fb = probe.choose_transport(os.path.abspath(__file__), requested,
                                           timeout_s=float(os.environ.get("FEDMX_PROBE_TIMEOUT_S", "180")))
-        os.environ.update(probe.TRANSPORT_ENV[used])
+        probe.apply_env(os.environ, used)
         _TRANSPORT["used"], _TRANSPORT["fallback"] = used, fb
         if fb is not None and os.environ.get("RANK") == "0":
             print(f"transport fallback: {requested} -> {used}: {fb['failures']}", file=sys.stderr)

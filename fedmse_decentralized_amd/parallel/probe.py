@@ -31,8 +31,9 @@ from typing import Dict, List, Optional, Tuple
 
 FALLBACK = ("rccl", "ipc", "gloo")
 # environment of each transport for the job and its probe
+# (None: removed, so the backend is the device's default -- nccl on GPUs)
 TRANSPORT_ENV = {
-    "rccl": {"FEDMX_COMM": "rccl"},
+    "rccl": {"FEDMX_COMM": "rccl", "FEDMX_DIST_BACKEND": None},
     "ipc": {"FEDMX_COMM": "ipc", "FEDMX_DIST_BACKEND": "gloo"},
     "gloo": {"FEDMX_COMM": "rccl", "FEDMX_DIST_BACKEND": "gloo"},
 }
@@ -60,10 +61,28 @@ def _store(world: int, timeout_s: float):
     return dist.PrefixStore("fedmx_probe", base)
 
 
+def apply_env(env, transport: str) -> None:
+    for k, v in TRANSPORT_ENV[transport].items():
+        if v is None:
+            env.pop(k, None)
+        else:
+            env[k] = v
+
+
+def requested_transport(comm_flag: Optional[str]) -> str:
+    """--comm, else FEDMX_COMM, else gloo when FEDMX_DIST_BACKEND=gloo (one-GPU
+    rehearsals), else rccl."""
+    if comm_flag:
+        return comm_flag
+    if os.environ.get("FEDMX_COMM"):
+        return os.environ["FEDMX_COMM"]
+    return "gloo" if os.environ.get("FEDMX_DIST_BACKEND") == "gloo" else "rccl"
+
+
 def run_child(transport: str, script: str, port: int, timeout_s: float) -> Tuple[int, str]:
     """This rank's probe of ``transport`` in a child process: (exit code, tail of its output)."""
     env = dict(os.environ)
-    env.update(TRANSPORT_ENV[transport])
+    apply_env(env, transport)
     env["MASTER_PORT"] = str(port)
     env["MASTER_ADDR"] = "127.0.0.1"
     # the child's own rendezvous: rank 0's child hosts the store

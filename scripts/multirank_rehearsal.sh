@@ -1,9 +1,12 @@
 #!/bin/bash
 # Multi-rank rehearsal of bench.py / main.py on a ONE-GPU box: NRANKS ranks
-# (default 2, at most 8 here) share
-# cuda:0 over the gloo backend (RCCL refuses duplicate GPUs).  Exercises the
-# sharded federation, the device-resident protocol's collectives and the
-# bench JSON contract (max over ranks) end to end.
+# (default 2, at most 8 here) share cuda:0 (RCCL refuses duplicate GPUs):
+# COMM=gloo (default) runs the round's collectives over gloo, COMM=ipc over
+# the peer-memory kernels (parallel/ipc.py; gloo only for bring-up), the
+# transport of the 8-GPU job's fallback (parallel/probe.py), which probes it
+# first here too.  Exercises the sharded federation, the device-resident
+# protocol's collectives and the bench JSON contract (max over ranks) end to
+# end; the bench record lands in gpurun_out/rehearsal_bench$NRANKS_$COMM.json.
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out
@@ -11,9 +14,12 @@ mkdir -p "$OUT"
 NR=${NRANKS:-2}
 [ "$NR" -ge 2 ] && [ "$NR" -le 8 ] || { echo "NRANKS must be 2..8"; exit 2; }
 export FEDMX_DEVICE_INDEX=0 FEDMX_DIST_BACKEND=gloo HSA_ENABLE_IPC_MODE_LEGACY=0
-python -c "import fedmse_decentralized_amd.ops.build as b; b.build_all()" || exit 3
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $NR --master-addr 127.0.0.1 \
-  --master-port 29517 bench.py --gpus $NR --steps 10 --warmup 2 > "$OUT/rehearsal_bench$NR.log" 2>&1
+COMM=${COMM:-gloo}
+CARG=""
+[ "$COMM" = ipc ] && CARG="--comm ipc"
+timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $NR --master-addr 127.0.0.1 \
+  --master-port 29517 bench.py --gpus $NR --steps ${STEPS:-20} --warmup 5 $CARG \
+  --out "$OUT/rehearsal_bench${NR}_$COMM.json" > "$OUT/rehearsal_bench$NR.log" 2>&1
 rc=$?
 echo "bench $NR ranks rc=$rc"; tail -n 3 "$OUT/rehearsal_bench$NR.log"
 [ $rc -ne 0 ] && exit $rc
