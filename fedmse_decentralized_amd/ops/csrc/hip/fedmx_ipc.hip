@@ -181,6 +181,9 @@ int fedmx_ipc_alloc(size_t bytes, void** ptr, void* handle_out) {
   if (e != hipSuccess) {
     (void)hipFree(*ptr);
     *ptr = nullptr;
+    // a failed HIP call stays the thread's "last error": torch would report it
+    // at its next unrelated call (the 8-process rehearsal's extras did)
+    (void)hipGetLastError();
   }
   return (int)e;
 }
@@ -189,7 +192,9 @@ int fedmx_ipc_open(const void* handle, void** ptr) {
   hipIpcMemHandle_t h;
   memcpy(&h, handle, sizeof h);
   *ptr = nullptr;
-  return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+  const hipError_t e = hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) (void)hipGetLastError();
+  return (int)e;
 }
 
 int fedmx_ipc_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }

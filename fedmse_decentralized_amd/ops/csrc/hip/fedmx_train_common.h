@@ -423,7 +423,7 @@ __device__ __forceinline__ void global_to_masters_o(const float* __restrict__ sr
 }
 
 // CLEAR_BU: the helper-wave kernel's in-launch bias units (the last element
-// of W1, W2 and W3, fedmx_train_hw.hip FEDMX_HW_BIAS_UNITS) are written as 0
+// of W1, W2, W3 and W4, fedmx_train_hw.hip FEDMX_HW_BIAS_UNITS) are written as 0
 template <bool CP, bool CLEAR_BU = false>
 __device__ __forceinline__ void masters_to_global_o(float* __restrict__ dst, float* sW1, float* sW4, float* sW2,
                                                     float* sW3) {
@@ -438,7 +438,8 @@ __device__ __forceinline__ void masters_to_global_o(float* __restrict__ dst, flo
 #pragma unroll
       for (int i = 0; i < 4; ++i) val[k][i] = *master_slot<CP>(e, i, sW1, sW4, sW2, sW3);
     }
-    if (CLEAR_BU && (e == OFF_W1 + HP * DP - 4 || e == OFF_W2 + ZP * HP - 4 || e == OFF_W3 + HP * ZP - 4))
+    if (CLEAR_BU && (e == OFF_W1 + HP * DP - 4 || e == OFF_W2 + ZP * HP - 4 || e == OFF_W3 + HP * ZP - 4 ||
+                     e == OFF_W4 + DP * HP - 4))
       val[k][3] = 0.f;
   }
 #pragma unroll

@@ -74,12 +74,26 @@
 // themselves instead of being set by a select after every product: inside
 // the launch W1's bias row, W2's bias row and W3's bias row hold a single 1
 // (in the input-bias column, the H1-bias column and the Z-bias column), so
-// relu(1 * 1) = 1, 1 * 1 = 1 and relu(1 * 1) = 1 exactly.  Their gradients
-// are zero (the dH1 / dZ / dH3 masks already exclude the bias slots), so Adam
+// relu(1 * 1) = 1, 1 * 1 = 1 and relu(1 * 1) = 1 exactly; W4's row of the
+// input-bias "feature" holds a 1 in the H3-bias column, so X's constant-1
+// column is reconstructed exactly and needs no mask in the loss and dY.
+// Their gradients are zero (the dH1 / dZ / dH3 masks already exclude the
+// bias slots; the bias feature's dY is exactly 0), so Adam
 // never moves them; the global parameters (aggregation, checkpoints) never
 // see them: set on staging in, cleared on staging out (bias_units_*).
+//
+// These three switches are bit masks over the kernel's instantiations -- bit
+// 0: batch <= 12 without FedProx (the benchmark's), bit 1: batch <= 12 with
+// FedProx, bit 2: MULTI (batch > 12, either) -- because the same removal of
+// VALU work measured faster in one and slower in another (r5 A/B, one box,
+// two passes, train launch us: plain / FedProx / batch 64):
+//   scaled Adam only       885.5 / 973 / 698.5
+//   + bias units + masks   900.5 / 953 / 680
+//   + ping-pong            877.5 / 977 / 696.5
+//   + all three            889   / 986 / 661
+// so each instantiation gets its fastest combination.
 #ifndef FEDMX_HW_BIAS_UNITS
-#define FEDMX_HW_BIAS_UNITS 1
+#define FEDMX_HW_BIAS_UNITS 6
 #endif
 // 1: the backward masks test values, not slot tables: every padded hidden /
 // latent slot holds exactly 0 (zero weights, relu(0) = 0, zero gradients),
@@ -88,7 +102,13 @@
 // excludes: one compare + select per element instead of compare + scalar AND
 // + select, and no select at all on the latent axis but the bias slot's
 #ifndef FEDMX_HW_VALUE_MASKS
-#define FEDMX_HW_VALUE_MASKS 1
+#define FEDMX_HW_VALUE_MASKS 6
+#endif
+// 1: the step loop unrolled by two with the current / prefetched chunk
+// buffers swapping roles (instead of copying the prefetched chunk's 16
+// registers into the current one after every step)
+#ifndef FEDMX_HW_PINGPONG
+#define FEDMX_HW_PINGPONG 5
 #endif
 // the same switch for the FedProx instantiation: 1 there (r4 A/B: FedProx
 // launch -3.3 %, the plain launch +6 % -- without FedProx the helpers' path is
@@ -166,12 +186,16 @@ struct HSlab {
 constexpr int BU_W1 = (OFF_W1 + HP * DP - 4) / 4;
 constexpr int BU_W2 = (OFF_W2 + ZP * HP - 4) / 4;
 constexpr int BU_W3 = (OFF_W3 + HP * ZP - 4) / 4;
+// and W4's row for the input-bias "feature" DP-1, H3-bias column: the
+// reconstruction of X's constant-1 column is then exactly 1, so its error
+// (and its dY, and its gradient) is 0 without a select
+constexpr int BU_W4 = (OFF_W4 + DP * HP - 4) / 4;
 // staging thread's share (stage_load layout): mark / clear the bias units
 __device__ __forceinline__ void bias_units_set(f32x4 (&val)[STAGE_PER_THREAD], float one) {
 #pragma unroll
   for (int k = 0; k < STAGE_PER_THREAD; ++k) {
     const int q = threadIdx.x + 256 * k;
-    if (q == BU_W1 || q == BU_W2 || q == BU_W3) val[k][3] = one;
+    if (q == BU_W1 || q == BU_W2 || q == BU_W3 || q == BU_W4) val[k][3] = one;
   }
 }
 
@@ -254,6 +278,11 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   constexpr bool CPB = !MULTI;       // compact batch order (12 rows of 16 columns)
   constexpr int KB = CPB ? 3 : 4;    // k-steps of products over the batch
   constexpr int KZ = 2;   // k-steps of products over the latent axis
+  // this instantiation's bit in the FEDMX_HW_{BIAS_UNITS,VALUE_MASKS,PINGPONG} masks
+  constexpr int ROLE = MULTI ? 4 : (PROX ? 2 : 1);
+  constexpr bool BU = (FEDMX_HW_BIAS_UNITS & ROLE) != 0;
+  constexpr bool VMASK = (FEDMX_HW_VALUE_MASKS & ROLE) != 0;
+  constexpr bool PPONG = (FEDMX_HW_PINGPONG & ROLE) != 0;
   __shared__ __attribute__((aligned(16))) float lds[L_TOTAL];
   const int w8 = threadIdx.x >> 6;
   const bool helper = w8 >= 4;
@@ -481,8 +510,8 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v0 = relu(sum0[r]), v1 = relu(sum1[r]);
-        if (!FEDMX_HW_BIAS_UNITS && hbias_d[0][r]) v0 = 1.f;
-        if (!FEDMX_HW_BIAS_UNITS && hbias_d[1][r]) v1 = 1.f;
+        if (!BU && hbias_d[0][r]) v0 = 1.f;
+        if (!BU && hbias_d[1][r]) v1 = 1.f;
         sum0[r] = v0;
         sum1[r] = v1;
       }
@@ -493,7 +522,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     f32x4 zb = z;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (!FEDMX_HW_BIAS_UNITS && zbias_d[r]) zb[r] = 1.f;
+      if (!BU && zbias_d[r]) zb[r] = 1.f;
     f32x4 h3[2];
     {
       f32x4 acc0 = zero4(), acc1 = zero4();
@@ -507,8 +536,8 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v0 = relu(acc0[r]), v1 = relu(acc1[r]);
-        if (!FEDMX_HW_BIAS_UNITS && hbias_d[0][r]) v0 = 1.f;
-        if (!FEDMX_HW_BIAS_UNITS && hbias_d[1][r]) v1 = 1.f;
+        if (!BU && hbias_d[0][r]) v0 = 1.f;
+        if (!BU && hbias_d[1][r]) v1 = 1.f;
         acc0[r] = v0;
         acc1[r] = v1;
       }
@@ -516,7 +545,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       h3[1] = acc1;
     }
     float nz = 0.f;
-    if (FEDMX_HW_VALUE_MASKS) {
+    if (VMASK) {
       // (padded latent slots are 0; the bias slot is row (g, r) = (3, 1))
       nz = z[0] * z[0] + (z_bias_lane ? 0.f : z[1] * z[1]) + z[2] * z[2] + z[3] * z[3];
     } else {
@@ -547,7 +576,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float d0 = acc0[r] - xf[b][0][r];
-        const float d1 = (b == 3 && g == 3 && r == 3) ? 0.f : acc1[r] - xf[b][1][r];
+        const float d1 = (!BU && b == 3 && g == 3 && r == 3) ? 0.f : acc1[r] - xf[b][1][r];
         sq += d0 * d0 + d1 * d1;
       }
       sq = ok ? sq : 0.f;
@@ -634,7 +663,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       min_valid = valid_loss;
       best_ep = ep;
       worse = 0;
-      if (stager) masters_to_global_o<CP, FEDMX_HW_BIAS_UNITS>(Bg, sW1, sW4, sW2, sW3);  // save_model(): best snapshot
+      if (stager) masters_to_global_o<CP, BU>(Bg, sW1, sW4, sW2, sW3);  // save_model(): best snapshot
     } else {
       ++worse;
     }
@@ -653,7 +682,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     stage_load(Vg, pv_v);
     if (PROX) stage_load(A.anchor + (size_t)cid * P_PAD, pv_a);
     stage_load(Pg, pv_p);
-    if (FEDMX_HW_BIAS_UNITS) {
+    if (BU) {
       bias_units_set(pv_p, 1.f);
       if (PROX) bias_units_set(pv_a, 1.f);   // (p - anchor = 0 there: no proximal pull)
     }
@@ -896,7 +925,10 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     }
     int mb = 0, mch = 0;   // MULTI: batch / chunk of this step
     f32x4 G1[2][2], Go;
-    for (int bi = 0; bi < nsteps; ++bi) {
+    // one training step on chunk `cur`, prefetching into `nxt`; the loop runs
+    // it twice per iteration with the two chunk buffers' roles swapped (no
+    // 16-register copy of the prefetched chunk per step: FEDMX_HW_PINGPONG)
+    auto train_step = [&](const int bi, XChunk& cur, XChunk& nxt) {
       // MULTI: this step is chunk mch of batch mb (16 rows from row_b); the
       // batch's row count bt sets the scales, the chunk's bc the masks
       const int row_b = MULTI ? mb * B + 16 * mch : bi * B;
@@ -973,7 +1005,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float vv = relu(s[r]);
-            if (!FEDMX_HW_BIAS_UNITS && hbias_d[t][r]) vv = 1.f;
+            if (!BU && hbias_d[t][r]) vv = 1.f;
             s[r] = vv;
           }
           h1[t] = s;
@@ -983,7 +1015,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         zb = z;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (!FEDMX_HW_BIAS_UNITS && zbias_d[r]) zb[r] = 1.f;
+          if (!BU && zbias_d[r]) zb[r] = 1.f;
         {
           f32x4 acc0 = zero4(), acc1 = zero4();
           const f32x4 a0 = lds_read4(a3p);
@@ -996,8 +1028,8 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v0 = relu(acc0[r]), v1 = relu(acc1[r]);
-            if (!FEDMX_HW_BIAS_UNITS && hbias_d[0][r]) v0 = 1.f;
-            if (!FEDMX_HW_BIAS_UNITS && hbias_d[1][r]) v1 = 1.f;
+            if (!BU && hbias_d[0][r]) v0 = 1.f;
+            if (!BU && hbias_d[1][r]) v1 = 1.f;
             acc0[r] = v0;
             acc1[r] = v1;
           }
@@ -1032,13 +1064,13 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float d0 = y[0][r] - cur.f0[r];
-          const float d1 = (bias_lane && r == 3) ? 0.f : y[1][r] - cur.f1[r];
+          const float d1 = (!BU && bias_lane && r == 3) ? 0.f : y[1][r] - cur.f1[r];
           sq += d0 * d0 + d1 * d1;
         }
         const bool col_ok = (unsigned)brow_c < (unsigned)bc;
         sq = col_ok ? sq : 0.f;
         float nz = 0.f;
-        if (FEDMX_HW_VALUE_MASKS) {
+        if (VMASK) {
           nz = z[0] * z[0] + (z_bias_lane ? 0.f : z[1] * z[1]) + z[2] * z[2] + z[3] * z[3];
         } else {
 #pragma unroll
@@ -1069,7 +1101,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         dy[0][r] = (y[0][r] - cur.f0[r]) * scale;
-        dy[1][r] = (bias_lane && r == 3) ? 0.f : (y[1][r] - cur.f1[r]) * scale;
+        dy[1][r] = (!BU && bias_lane && r == 3) ? 0.f : (y[1][r] - cur.f1[r]) * scale;
         sT0[tw + r * S_T] = dy[0][r];
         sT0[tw + (16 + r) * S_T] = dy[1][r];
         sT1[tw + r * S_T] = h3[0][r];
@@ -1114,7 +1146,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if (FEDMX_HW_VALUE_MASKS)
+          if (VMASK)
             s[r] = (h3[t][r] > ((t == 1 && r == 2) ? thr_h3b : 0.f)) ? s[r] : 0.f;
           else
             s[r] = (hreal_d[t][r] && h3[t][r] > 0.f) ? s[r] : 0.f;
@@ -1134,7 +1166,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       const float shr = (col_ok && norm_c > 0.f) ? shr_raw : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (FEDMX_HW_VALUE_MASKS)
+        if (VMASK)
           dz[r] = (r == 1 && z_bias_lane) ? 0.f : dz[r] + shr * z[r];
         else
           dz[r] = zreal_d[r] ? dz[r] + shr * z[r] : 0.f;
@@ -1152,7 +1184,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         for (int s = 0; s < KZ; ++s) acc = mfma16(dz[s], q2[t][s], acc);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if (FEDMX_HW_VALUE_MASKS)
+          if (VMASK)
             acc[r] = (h1b[t][r] > (t == 1 ? thr_h1b : 0.f)) ? acc[r] : 0.f;
           else
             acc[r] = (hreal_c[t] && h1b[t][r] > 0.f) ? acc[r] : 0.f;
@@ -1219,7 +1251,19 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #if FEDMX_HW_IGLP >= 0
       __builtin_amdgcn_iglp_opt(FEDMX_HW_IGLP);
 #endif
-      cur = nxt;
+    };
+    if constexpr (PPONG) {
+      int bi = 0;
+      for (; bi + 1 < nsteps; bi += 2) {
+        train_step(bi, cur, nxt);
+        train_step(bi + 1, nxt, cur);
+      }
+      if (bi < nsteps) train_step(bi, cur, nxt);
+    } else {
+      for (int bi = 0; bi < nsteps; ++bi) {
+        train_step(bi, cur, nxt);
+        cur = nxt;
+      }
     }
     w1_to_lds(P, L);   // W1 master (validation, snapshot)
     double prox_now = 0.0;
@@ -1247,7 +1291,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // ---- write back: params (masters), then m and v through the same staging
   HSTAMP(true, 30);
   __syncthreads();
-  masters_to_global_o<CP, FEDMX_HW_BIAS_UNITS>(Pg, sW1, sW4, sW2, sW3);
+  masters_to_global_o<CP, BU>(Pg, sW1, sW4, sW2, sW3);
   if (FEDMX_HW_SCALED) {
     scale_mslab(M, K.one_m_b1);
     scale_mslab(V, K.one_m_b2);

@@ -68,7 +68,16 @@ class _Channel:
         hsz = self.L.fedmx_ipc_handle_size()
         handle = (ctypes.c_uint8 * hsz)()
         p = ctypes.c_void_p()
-        rc = self.L.fedmx_ipc_alloc(nbytes, ctypes.byref(p), ctypes.cast(handle, ctypes.c_void_p))
+        # (retried locally: with several processes sharing one GPU an export
+        # has failed transiently, hipErrorInvalidValue on one rank of 8)
+        for attempt in range(3):
+            rc = self.L.fedmx_ipc_alloc(nbytes, ctypes.byref(p), ctypes.cast(handle, ctypes.c_void_p))
+            if rc == 0:
+                break
+            log.warning(f"rank {me}: receive-area allocation / export failed (code {rc}), attempt {attempt + 1}")
+            import time
+
+            time.sleep(0.2 * (attempt + 1))
         self.own = p.value if rc == 0 else None
         allh = comm.base_all_gather_object((rc, bytes(handle)))
         bad = [r for r, (c, _) in enumerate(allh) if c != 0]

@@ -26,7 +26,9 @@ VARIANTS = {
     # hwsplitd1/2) and grouped dH3 reads (red8) measured slower and were removed from
     # the kernel (profiles/r4_train_hw_experiments.md; source in git history, commit ef22669)
     "hwscaled0": ["-DFEDMX_HW_SCALED=0"],           # r5: unscaled FMA Adam in the helper-wave kernel: 897 vs 870 us (-3.0 %)
-    "nobu": ["-DFEDMX_HW_BIAS_UNITS=0", "-DFEDMX_HW_VALUE_MASKS=0"],   # r5: bias slots by select, slot-table masks
+    # r5: per-instantiation masks (bit 0 plain batch <= 12, 1 FedProx, 2 batch > 12); default 6 / 6 / 5
+    "allon": ["-DFEDMX_HW_BIAS_UNITS=7", "-DFEDMX_HW_VALUE_MASKS=7", "-DFEDMX_HW_PINGPONG=7"],
+    "r5base": ["-DFEDMX_HW_BIAS_UNITS=0", "-DFEDMX_HW_VALUE_MASKS=0", "-DFEDMX_HW_PINGPONG=0"],   # scaled Adam only
     "exact": ["-DFEDMX_EXACT_ADAM=1"],               # r4: IEEE sqrt / division Adam (torch's op sequence)
     "flags": ["-DFEDMX_HW_FLAGS=1"],                 # r4: mains-only layer-1 exchange + helper->main LDS flags
     "flags_madam": ["-DFEDMX_HW_FLAGS=1", "-DFEDMX_HW_ABLATE=32"],   # timing only: + mains skip W1 Adam

@@ -14,6 +14,8 @@ mkdir -p "$OUT"
 NR=${NRANKS:-2}
 [ "$NR" -ge 2 ] && [ "$NR" -le 8 ] || { echo "NRANKS must be 2..8"; exit 2; }
 export FEDMX_DEVICE_INDEX=0 FEDMX_DIST_BACKEND=gloo HSA_ENABLE_IPC_MODE_LEGACY=0
+# the extras' watchdog well inside gpurun's 180 s silence limit
+export FEDMX_BENCH_EXTRA_TIMEOUT_S=${FEDMX_BENCH_EXTRA_TIMEOUT_S:-150}
 COMM=${COMM:-gloo}
 CARG=""
 [ "$COMM" = ipc ] && CARG="--comm ipc"
