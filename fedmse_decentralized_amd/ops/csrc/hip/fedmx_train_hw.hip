@@ -110,6 +110,9 @@
 #ifndef FEDMX_HW_PINGPONG
 #define FEDMX_HW_PINGPONG 5
 #endif
+#ifndef FEDMX_SPLIT_CHAINS
+#define FEDMX_SPLIT_CHAINS 0
+#endif
 // the same switch for the FedProx instantiation: 1 there (r4 A/B: FedProx
 // launch -3.3 %, the plain launch +6 % -- without FedProx the helpers' path is
 // short enough that the flag polls only add latency to the mains')
@@ -246,13 +249,28 @@ __device__ __forceinline__ void lds_to_hslab(HSlab& o, const Lane& L) {
       for (int v = 0; v < 2; ++v) o.q4[v][t][r] = L.w4[(16 * v + r) * S_W4 + 16 * t];
 }
 
-// compact-order product over the two halves of the hidden axis (7 k-steps)
+// compact-order product over the two halves of the hidden axis (7 k-steps).
+// FEDMX_SPLIT_CHAINS (fedmx_train.hip, the same switch and order there): each
+// half in its own accumulator, interleaved, then added -- a 4-long dependent
+// MFMA chain instead of 7 (40-cycle result latency vs 32-cycle issue) on the
+// main waves' serial path (z after barrier #1, dZ after barrier #2)
 __device__ __forceinline__ f32x4 chain2(f32x4 a0, f32x4 a1, f32x4 b0, f32x4 b1) {
   f32x4 x = zero4();
+#if FEDMX_SPLIT_CHAINS
+  f32x4 y = zero4();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    x = mfma16(a0[s], b0[s], x);
+    if (s < 3) y = mfma16(a1[s], b1[s], y);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) x[r] = x[r] + y[r];
+#else
 #pragma unroll
   for (int s = 0; s < 4; ++s) x = mfma16(a0[s], b0[s], x);
 #pragma unroll
   for (int s = 0; s < 3; ++s) x = mfma16(a1[s], b1[s], x);
+#endif
   return x;
 }
 
