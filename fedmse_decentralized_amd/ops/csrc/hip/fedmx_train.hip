@@ -182,29 +182,32 @@ __device__ __forceinline__ void scale_slab(Slab& o, float f) {
 // 16x16 product summed over the two 16-wide halves of the hidden axis
 // (k-steps (t, s)): L2 (W2a H1) and dZ (W3a^T dH3).  These are the dependent
 // chains on the step's critical path (one accumulator: 7-8 x 40-cycle MFMA
-// latency); FEDMX_SPLIT_CHAINS sums each half in its own accumulator and adds
-// the two, so the chain is ~half as long.
+// latency); SPLIT sums each half in its own accumulator and adds the two, so
+// the chain is ~half as long.  FEDMX_SPLIT_CHAINS is a mask over the
+// instantiations (bit 0 plain, bit 1 FedProx), defined with
+// fedmx_train_hw.hip's (whose bit 2, batch > 12, has no instantiation of its
+// own here) so that the two kernels sum in the same order.
 #ifndef FEDMX_SPLIT_CHAINS
-#define FEDMX_SPLIT_CHAINS 0
+#define FEDMX_SPLIT_CHAINS 5
 #endif
-template <bool CP>
+template <bool CP, bool SPLIT>
 __device__ __forceinline__ f32x4 chain2(f32x4 a0, f32x4 a1, f32x4 b0, f32x4 b1) {
   f32x4 x = zero4();
-#if FEDMX_SPLIT_CHAINS
-  f32x4 y = zero4();
+  if (SPLIT) {
+    f32x4 y = zero4();
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    x = mfma16(a0[s], b0[s], x);
-    if (s < (CP ? 3 : 4)) y = mfma16(a1[s], b1[s], y);
+    for (int s = 0; s < 4; ++s) {
+      x = mfma16(a0[s], b0[s], x);
+      if (s < (CP ? 3 : 4)) y = mfma16(a1[s], b1[s], y);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[r] = x[r] + y[r];
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) x = mfma16(a0[s], b0[s], x);
+#pragma unroll
+    for (int s = 0; s < (CP ? 3 : 4); ++s) x = mfma16(a1[s], b1[s], x);
   }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) x[r] = x[r] + y[r];
-#else
-#pragma unroll
-  for (int s = 0; s < 4; ++s) x = mfma16(a0[s], b0[s], x);
-#pragma unroll
-  for (int s = 0; s < (CP ? 3 : 4); ++s) x = mfma16(a1[s], b1[s], x);
-#endif
   return x;
 }
 
@@ -230,6 +233,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   static_assert(ONE || !CP, "compact order needs single-tile batches");
   constexpr int KB = CP ? 3 : 4;   // k-steps of products over the batch
   constexpr int KZ = CP ? 2 : 4;   // k-steps of products over the latent axis
+  constexpr bool SPLIT = (FEDMX_SPLIT_CHAINS & (PROX ? 2 : 1)) != 0;
   __shared__ __attribute__((aligned(16))) float lds[L_TOTAL];
   const int w = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -428,7 +432,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       h1[t] = s;
     }
     parity ^= 1;
-    z = chain2<CP>(lds_read4(a2p), lds_read4(a2p + 16), h1[0], h1[1]);
+    z = chain2<CP, SPLIT>(lds_read4(a2p), lds_read4(a2p + 16), h1[0], h1[1]);
     zb = z;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -552,7 +556,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       h1[0] = sum0;
       h1[1] = sum1;
     }
-    const f32x4 z = chain2<CP>(lds_read4(a2p), lds_read4(a2p + 16), h1[0], h1[1]);
+    const f32x4 z = chain2<CP, SPLIT>(lds_read4(a2p), lds_read4(a2p + 16), h1[0], h1[1]);
     f32x4 zb = z;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -813,7 +817,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         for (int r = 0; r < 4; ++r) sT0[tw + (16 * t + r) * S_T] = dh3[t][r];
       // ---- dZ = W3a^T dH3 (pre-update W3, every wave), + shrink-loss gradient
       //      lambda/B * z / ||z|| (0 where ||z|| == 0)
-      f32x4 dz = chain2<CP>(f32x4{q3[0][0], q3[0][1], q3[0][2], q3[0][3]},
+      f32x4 dz = chain2<CP, SPLIT>(f32x4{q3[0][0], q3[0][1], q3[0][2], q3[0][3]},
                             f32x4{q3[1][0], q3[1][1], q3[1][2], q3[1][3]}, dh3[0], dh3[1]);
       const float shr_raw = lam * __builtin_amdgcn_rcpf((float)bt * norm_c);
       const float shr = (col_ok && norm_c > 0.f) ? shr_raw : 0.f;

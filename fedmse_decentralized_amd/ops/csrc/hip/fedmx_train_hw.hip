@@ -110,8 +110,11 @@
 #ifndef FEDMX_HW_PINGPONG
 #define FEDMX_HW_PINGPONG 5
 #endif
+// the L2 / dZ products as two accumulator chains (chain2 below; the same
+// mask in fedmx_train.hip keeps the two kernels bit-identical).  r5h A/B:
+// plain -0.7 %, batch 64 -0.3 %, FedProx +1.2 % (profiles/r5_train_kernel_ab.md)
 #ifndef FEDMX_SPLIT_CHAINS
-#define FEDMX_SPLIT_CHAINS 0
+#define FEDMX_SPLIT_CHAINS 5
 #endif
 // the same switch for the FedProx instantiation: 1 there (r4 A/B: FedProx
 // launch -3.3 %, the plain launch +6 % -- without FedProx the helpers' path is
@@ -250,27 +253,29 @@ __device__ __forceinline__ void lds_to_hslab(HSlab& o, const Lane& L) {
 }
 
 // compact-order product over the two halves of the hidden axis (7 k-steps).
-// FEDMX_SPLIT_CHAINS (fedmx_train.hip, the same switch and order there): each
-// half in its own accumulator, interleaved, then added -- a 4-long dependent
-// MFMA chain instead of 7 (40-cycle result latency vs 32-cycle issue) on the
-// main waves' serial path (z after barrier #1, dZ after barrier #2)
+// SPLIT (FEDMX_SPLIT_CHAINS, per instantiation; fedmx_train.hip the same
+// order): each half in its own accumulator, interleaved, then added -- a
+// 4-long dependent MFMA chain instead of 7 (40-cycle result latency vs
+// 32-cycle issue) on the main waves' serial path (z after barrier #1, dZ
+// after barrier #2)
+template <bool SPLIT>
 __device__ __forceinline__ f32x4 chain2(f32x4 a0, f32x4 a1, f32x4 b0, f32x4 b1) {
   f32x4 x = zero4();
-#if FEDMX_SPLIT_CHAINS
-  f32x4 y = zero4();
+  if (SPLIT) {
+    f32x4 y = zero4();
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    x = mfma16(a0[s], b0[s], x);
-    if (s < 3) y = mfma16(a1[s], b1[s], y);
+    for (int s = 0; s < 4; ++s) {
+      x = mfma16(a0[s], b0[s], x);
+      if (s < 3) y = mfma16(a1[s], b1[s], y);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[r] = x[r] + y[r];
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) x = mfma16(a0[s], b0[s], x);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) x = mfma16(a1[s], b1[s], x);
   }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) x[r] = x[r] + y[r];
-#else
-#pragma unroll
-  for (int s = 0; s < 4; ++s) x = mfma16(a0[s], b0[s], x);
-#pragma unroll
-  for (int s = 0; s < 3; ++s) x = mfma16(a1[s], b1[s], x);
-#endif
   return x;
 }
 
@@ -301,6 +306,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   constexpr bool BU = (FEDMX_HW_BIAS_UNITS & ROLE) != 0;
   constexpr bool VMASK = (FEDMX_HW_VALUE_MASKS & ROLE) != 0;
   constexpr bool PPONG = (FEDMX_HW_PINGPONG & ROLE) != 0;
+  constexpr bool SPLIT = (FEDMX_SPLIT_CHAINS & ROLE) != 0;
   __shared__ __attribute__((aligned(16))) float lds[L_TOTAL];
   const int w8 = threadIdx.x >> 6;
   const bool helper = w8 >= 4;
@@ -536,7 +542,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       h1[0] = sum0;
       h1[1] = sum1;
     }
-    const f32x4 z = chain2(lds_read4(a2p), lds_read4(a2p + 16), h1[0], h1[1]);
+    const f32x4 z = chain2<SPLIT>(lds_read4(a2p), lds_read4(a2p + 16), h1[0], h1[1]);
     f32x4 zb = z;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -1029,7 +1035,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           h1[t] = s;
         }
         parity ^= 1;
-        z = chain2(lds_read4(a2p), lds_read4(a2p + 16), h1[0], h1[1]);
+        z = chain2<SPLIT>(lds_read4(a2p), lds_read4(a2p + 16), h1[0], h1[1]);
         zb = z;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -1178,7 +1184,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) sT2[tw + (16 * t + r) * S_T] = dh3[t][r];
       // ---- dZ = W3a^T dH3 (+ shrink-loss gradient)
-      f32x4 dz = chain2(f32x4{q3[0][0], q3[0][1], q3[0][2], q3[0][3]},
+      f32x4 dz = chain2<SPLIT>(f32x4{q3[0][0], q3[0][1], q3[0][2], q3[0][3]},
                         f32x4{q3[1][0], q3[1][1], q3[1][2], q3[1][3]}, dh3[0], dh3[1]);
       const float shr_raw = lam * __builtin_amdgcn_rcpf((float)bt * norm_c);
       const float shr = (col_ok && norm_c > 0.f) ? shr_raw : 0.f;

@@ -48,7 +48,8 @@ VARIANTS = {
     "hint1": ["-DFEDMX_SCHED_HINTS=1"],           # 64 x (1 MFMA, 6 VALU)      (+9%)
     "sepadam": ["-DFEDMX_ADAM_FMA=0"],            # separately rounded Adam    (+3%)
     "dw4late": ["-DFEDMX_DW4_LATE=1"],            # dW4 products after barrier #2 (+0.5%)
-    "split_chains": ["-DFEDMX_SPLIT_CHAINS=1"],   # L2 / dZ as two accumulator chains (4-wave kernel r2: +0.3 %; r5: both kernels)
+    "split_chains": ["-DFEDMX_SPLIT_CHAINS=7"],   # L2 / dZ as two accumulator chains everywhere (r5h: plain -0.7 %, b64 -0.3 %, FedProx +1.2 %: production mask 5)
+    "nosplit": ["-DFEDMX_SPLIT_CHAINS=0"],        # one accumulator chain everywhere (the round-5 r5g build)
     "novgprform": ["-mllvm", "-amdgpu-mfma-vgpr-form=0"],  # AGPR accumulators (+3.3%)
     "noslp": ["-fno-slp-vectorize"],              # no packed fp32 VALU        (+5%)
     "w4pos1": ["-DFEDMX_W4_POS=1"],               # W4 Adam after dH1, fenced   (+2.5%)
