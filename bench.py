@@ -460,7 +460,9 @@ def _main(argv, real_stdout: int):
         # every rank leaves, so the launcher sees the job end.
         import threading
 
-        limit = float(os.environ.get("FEDMX_BENCH_EXTRA_TIMEOUT_S", "600"))
+        # (the 8-rank extras took < 150 s with all ranks sharing ONE GPU: 300 s is
+        # ample on a node and keeps a stuck job well inside a driver time limit)
+        limit = float(os.environ.get("FEDMX_BENCH_EXTRA_TIMEOUT_S", "300"))
 
         def _give_up():
             if rec is not None:

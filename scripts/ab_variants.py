@@ -49,7 +49,12 @@ VARIANTS = {
     "sepadam": ["-DFEDMX_ADAM_FMA=0"],            # separately rounded Adam    (+3%)
     "dw4late": ["-DFEDMX_DW4_LATE=1"],            # dW4 products after barrier #2 (+0.5%)
     "split_chains": ["-DFEDMX_SPLIT_CHAINS=7"],   # L2 / dZ as two accumulator chains everywhere (r5h: plain -0.7 %, b64 -0.3 %, FedProx +1.2 %: production mask 5)
-    "nosplit": ["-DFEDMX_SPLIT_CHAINS=0"],        # one accumulator chain everywhere (the round-5 r5g build)
+    "nosplit": ["-DFEDMX_SPLIT_CHAINS=0"],
+    "early1": ["-DFEDMX_HW_EARLY_DW4=7"],         # helpers' dW4 MFMAs before barrier #2 (flag from main w)
+    "early2": ["-DFEDMX_HW_EARLY_ADAM=7"],        # helpers' dW4 + W4 Adam + publication before barrier #2
+    "early1p": ["-DFEDMX_HW_EARLY_DW4=7", "-DFEDMX_HW_MAIN_PRIO=2"],    # early1 with the mains at issue priority
+    "early2p": ["-DFEDMX_HW_EARLY_ADAM=7", "-DFEDMX_HW_MAIN_PRIO=2"],   # early2 with the mains at issue priority
+    "mainprio": ["-DFEDMX_HW_MAIN_PRIO=2"],       # mains at issue priority over their helpers        # one accumulator chain everywhere (the round-5 r5g build)
     "novgprform": ["-mllvm", "-amdgpu-mfma-vgpr-form=0"],  # AGPR accumulators (+3.3%)
     "noslp": ["-fno-slp-vectorize"],              # no packed fp32 VALU        (+5%)
     "w4pos1": ["-DFEDMX_W4_POS=1"],               # W4 Adam after dH1, fenced   (+2.5%)
