@@ -119,28 +119,6 @@
 // the same switch for the FedProx instantiation: 1 there (r4 A/B: FedProx
 // launch -3.3 %, the plain launch +6 % -- without FedProx the helpers' path is
 // short enough that the flag polls only add latency to the mains')
-// Helper start (masks over the instantiations, as above): a helper waits for
-// an LDS flag its main wave sets right after writing dY^T / H3^T, before the
-// main's dH3-partial MFMAs, instead of for barrier #2.  The helper's work then
-// runs in the forward half of the step, where the helpers idled (r5 stamps:
-// ~3,200 cycles of barrier-#2 wait per step) and the mains leave issue slots
-// free, instead of competing with the mains' backward chain after barrier #2.
-// EARLY_DW4: dW4's MFMAs before barrier #2 (W4's Adam and publication after
-// it, as before); EARLY_ADAM: W4's Adam and publication too.  Safe because
-// main w has read all of W4(s) (layer 4, the dH3 A-operand rows) and its Adam
-// scalars before it writes dY^T, and the helper publishes into the other
-// parity slot of the scalars.
-#ifndef FEDMX_HW_EARLY_DW4
-#define FEDMX_HW_EARLY_DW4 0
-#endif
-#ifndef FEDMX_HW_EARLY_ADAM
-#define FEDMX_HW_EARLY_ADAM 0
-#endif
-// static issue priority of the main waves over their helpers (s_setprio;
-// r2 measured +0.4 % with the barrier-#2 helper start)
-#ifndef FEDMX_HW_MAIN_PRIO
-#define FEDMX_HW_MAIN_PRIO 0
-#endif
 #ifndef FEDMX_HW_FLAGS_PROX
 #define FEDMX_HW_FLAGS_PROX 1
 #endif
@@ -329,8 +307,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   constexpr bool VMASK = (FEDMX_HW_VALUE_MASKS & ROLE) != 0;
   constexpr bool PPONG = (FEDMX_HW_PINGPONG & ROLE) != 0;
   constexpr bool SPLIT = (FEDMX_SPLIT_CHAINS & ROLE) != 0;
-  constexpr int EARLY = (FEDMX_HW_EARLY_ADAM & ROLE) ? 2 : ((FEDMX_HW_EARLY_DW4 & ROLE) ? 1 : 0);
-  static_assert(EARLY == 0 || HWF < 2, "the early helper start keeps barrier #2");
   __shared__ __attribute__((aligned(16))) float lds[L_TOTAL];
   const int w8 = threadIdx.x >> 6;
   const bool helper = w8 >= 4;
@@ -362,7 +338,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // [8..11] (FLAGS 2) dH3 partial + dY^T / H3^T of step count v written by main w
   int* const sFlag = reinterpret_cast<int*>(sK + 32);
   // [12]: OR of every wave's spin_fail, read by thread 0 after the last barrier
-  // [16..19] (EARLY) dY^T / H3^T of chunk sequence number v written by main w
   int* const sFail = sFlag + 12;
   bool spin_fail = false;
   auto flag_set = [&](int i, int v) {
@@ -724,7 +699,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // (m, v, [anchor], params) in one memory round trip, then each tensor
   // passes through the masters in turn (the barrier sequence of one global_to_masters_o pass per tensor)
   HSTAMP(true, 28);
-  if (threadIdx.x < 20) sFlag[threadIdx.x] = 0;   // flags + failure word (the staging barriers follow)
+  if (threadIdx.x < 13) sFlag[threadIdx.x] = 0;   // flags + failure word (the staging barriers follow)
   f32x4 pv_m[STAGE_PER_THREAD], pv_v[STAGE_PER_THREAD], pv_a[STAGE_PER_THREAD], pv_p[STAGE_PER_THREAD];
   if (stager) {
     stage_load(Mg, pv_m);
@@ -778,7 +753,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     // step when they computed them, FEDMX_HW_ABLATE=1) are formed here one
     // step ahead and handed over through LDS.
     int js = 0;   // step index within the launch
-    int fseq = 0;   // EARLY: chunk sequence number (main w's flag 16 + w)
     auto publish_k = [&]() {
       next_constants();
       const f32x4 kq = FEDMX_HW_SCALED ? f32x4{K.kd, K.ed, 0.f, 0.f} : f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f};
@@ -811,15 +785,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         HSTAMP(hs, 0);
         if (!HWF) __syncthreads();   // barrier #1 (main: layer-1 partials)
         HSTAMP(hs, 2);
-        if (EARLY)
-          flag_wait(16 + w, 1, ++fseq);  // main w's dY^T / H3^T of this chunk
-        else if (HWF >= 2)
+        if (HWF >= 2)
           flag_wait(8 + w, 1, js + 1);   // main w's dY^T / H3^T of this step
         else
           __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
         HSTAMP(hs, 7);
         if (FEDMX_HW_ABLATE & 64) {
-          if (EARLY) __syncthreads();   // barrier #2
           ++js;
           publish_k();
           if (HWF) flag_set(4 + w, js + 1);
@@ -842,7 +813,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           G4[1][0] = mfma16(w4a1[s], w4b0[s], G4[1][0]);
           G4[1][1] = mfma16(w4a1[s], w4b1[s], G4[1][1]);
         }
-        if (EARLY == 1 || (EARLY == 2 && !last_ch)) __syncthreads();   // barrier #2
         if (!last_ch) continue;   // MULTI: W4's Adam after the batch's last chunk
         HSTAMP(hs, 8);
 
@@ -875,7 +845,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         // launch must report itself failed)
         if (HWF && !((A.flags & TRAIN_FLAG_TEST_DROP_W4) && w == 0 && js == 3))
           flag_set(4 + w, js + 1);   // W4(js) ready for main w's layer 4
-        if (EARLY == 2) __syncthreads();   // barrier #2
         HSTAMP(hs, 11);
       }
       double prox_now = 0.0;
@@ -918,8 +887,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 
   // ============================= main waves =====================================
   int js = 0;   // step index within the launch (selects the Adam-scalar slot)
-  int fseq = 0;   // EARLY: chunk sequence number for helper w (flag 16 + w)
-  if (FEDMX_HW_MAIN_PRIO) __builtin_amdgcn_s_setprio(FEDMX_HW_MAIN_PRIO);
   MSlab P, M, V, AN;
   stage_vals(pv_m);
   lds_to_mslab(M, L);
@@ -1164,7 +1131,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         sT1[tw + r * S_T] = h3[0][r];
         sT1[tw + (16 + r) * S_T] = h3[1][r];
       }
-      if (EARLY) flag_set(16 + w, ++fseq);   // helper w may start on this chunk's dW4
       // ---- dH3 partial = W4a(own rows)^T dY(own rows)   (W4(s))
       {
         f32x4 acc0 = zero4(), acc1 = zero4();

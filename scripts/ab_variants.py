@@ -25,6 +25,8 @@ VARIANTS = {
     # r4: pipelined W1 Adam (pipe, flags_pipe, flags2_pipe), the SPLIT step (hwsplit,
     # hwsplitd1/2) and grouped dH3 reads (red8) measured slower and were removed from
     # the kernel (profiles/r4_train_hw_experiments.md; source in git history, commit ef22669)
+    # r5: the early helper start (early1/early2, +1.6 / +18 %) and main-wave priority
+    # (mainprio, +0.6 %) likewise (profiles/r5_train_kernel_ab.md; commit 247945c)
     "hwscaled0": ["-DFEDMX_HW_SCALED=0"],           # r5: unscaled FMA Adam in the helper-wave kernel: 897 vs 870 us (-3.0 %)
     # r5: per-instantiation masks (bit 0 plain batch <= 12, 1 FedProx, 2 batch > 12); default 6 / 6 / 5
     "allon": ["-DFEDMX_HW_BIAS_UNITS=7", "-DFEDMX_HW_VALUE_MASKS=7", "-DFEDMX_HW_PINGPONG=7"],
@@ -50,11 +52,6 @@ VARIANTS = {
     "dw4late": ["-DFEDMX_DW4_LATE=1"],            # dW4 products after barrier #2 (+0.5%)
     "split_chains": ["-DFEDMX_SPLIT_CHAINS=7"],   # L2 / dZ as two accumulator chains everywhere (r5h: plain -0.7 %, b64 -0.3 %, FedProx +1.2 %: production mask 5)
     "nosplit": ["-DFEDMX_SPLIT_CHAINS=0"],
-    "early1": ["-DFEDMX_HW_EARLY_DW4=7"],         # helpers' dW4 MFMAs before barrier #2 (flag from main w)
-    "early2": ["-DFEDMX_HW_EARLY_ADAM=7"],        # helpers' dW4 + W4 Adam + publication before barrier #2
-    "early1p": ["-DFEDMX_HW_EARLY_DW4=7", "-DFEDMX_HW_MAIN_PRIO=2"],    # early1 with the mains at issue priority
-    "early2p": ["-DFEDMX_HW_EARLY_ADAM=7", "-DFEDMX_HW_MAIN_PRIO=2"],   # early2 with the mains at issue priority
-    "mainprio": ["-DFEDMX_HW_MAIN_PRIO=2"],       # mains at issue priority over their helpers        # one accumulator chain everywhere (the round-5 r5g build)
     "novgprform": ["-mllvm", "-amdgpu-mfma-vgpr-form=0"],  # AGPR accumulators (+3.3%)
     "noslp": ["-fno-slp-vectorize"],              # no packed fp32 VALU        (+5%)
     "w4pos1": ["-DFEDMX_W4_POS=1"],               # W4 Adam after dH1, fenced   (+2.5%)
