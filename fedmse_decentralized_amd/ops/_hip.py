@@ -43,6 +43,9 @@ TRAIN_TEST_FLAGS = 0
 # unset: the library's build default
 _HELPER_ENV = os.environ.get("FEDMX_TRAIN_HELPER")
 TRAIN_HELPER = None if _HELPER_ENV is None else _HELPER_ENV != "0"
+# asynchronous validation of the helper-wave kernel (validator workgroups
+# beside the trainers, fedmx_train_hw.hip): "0" turns it off
+TRAIN_ASYNC_VALID = os.environ.get("FEDMX_TRAIN_ASYNC_VALID", "1") != "0"
 _lib = None
 _lib_path: Optional[Path] = None
 
@@ -76,7 +79,7 @@ class TrainArgs(ctypes.Structure):
         ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
         ("eps", ctypes.c_float), ("lam", ctypes.c_float), ("mu", ctypes.c_float),
         ("stamps", ctypes.c_void_p), ("flags", ctypes.c_int32), ("pad0", ctypes.c_int32),
-        ("err", ctypes.c_void_p),
+        ("err", ctypes.c_void_p), ("vws", ctypes.c_void_p), ("vseq", ctypes.c_uint32), ("pad1", ctypes.c_int32),
     ]
 
 
@@ -156,6 +159,8 @@ def lib():
                 "fedmx_copy2_f64": [vp, vp, i32, vp, vp, i32, vp],
                 "fedmx_copy_rows": [vp, i32, vp, vp, i32, vp, i32, i32, vp],
                 "fedmx_protocol_sizes": [vp],
+                "fedmx_train_av_slot": [],
+                "fedmx_train_hw_last_grid": [],
                 # one-shot peer-memory exchange (fedmx_ipc.hip, parallel/ipc.py)
                 "fedmx_ipc_alloc": [ctypes.c_size_t, ctypes.POINTER(vp), vp],
                 "fedmx_ipc_open": [vp, ctypes.POINTER(vp)],
@@ -718,10 +723,32 @@ class TrainBuffers:
             raise ValueError("training / validation buffers must hold 1 in column DP-1 (ClientStore._concat)")
         self.train_off = torch.from_numpy(store.train_off).to(dev)
         self.valid_off = torch.from_numpy(store.valid_off).to(dev)
+        self.dev = dev
+        self.vws: Optional[torch.Tensor] = None   # validator workspace [k][fedmx_train_av_slot()] (zeroed once)
+        self.vseq = 0                            # launch number stamped into its flags
+
+    def validator_workspace(self, k: int, n_rows: int):
+        """(pointer, launch number) of the asynchronous-validation workspace
+        for a k-client launch, or (None, 0) when k validators would not fit
+        beside their trainers.  Allocated once (one slot per client the
+        device can host a validator for, at most one per store row; never
+        freed, so no in-flight launch loses it) and never cleared again:
+        every launch stamps its flags with a new number, so stale flags of
+        earlier launches never match."""
+        if self.vws is None:
+            cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
+            self.vslots = max(0, min(int(n_rows), cus // 2))
+            self.vws = torch.zeros(max(self.vslots, 1) * int(lib().fedmx_train_av_slot()), dtype=torch.float32,
+                                   device=self.dev)
+        if k > self.vslots:
+            return None, 0
+        self.vseq = self.vseq % 0xFFFFFFFF + 1
+        return self.vws.data_ptr(), self.vseq
 
 
 def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tensor] = None,
-          compact: Optional[bool] = None, helper: Optional[bool] = None, err: int = 0):
+          compact: Optional[bool] = None, helper: Optional[bool] = None, err: int = 0,
+          async_valid: bool = True):
     """Launch the fused training kernel for store rows ``local_ids`` (async).
     Returns host views (tracking[k, E, 2], epochs_run[k], best_epoch[k])
     written by the kernel, valid after the next stream sync."""
@@ -759,6 +786,8 @@ def train(store, local_ids: Sequence[int], hp, dims, stamps: Optional[torch.Tens
     a.lam, a.mu = hp.shrink_lambda, hp.fedprox_mu
     a.stamps = stamps.data_ptr() if stamps is not None else None
     a.err = err or None
+    if TRAIN_ASYNC_VALID and async_valid:
+        a.vws, a.vseq = bufs.validator_workspace(k, store.params.shape[0])
     a.flags = 0 if (TRAIN_COMPACT if compact is None else compact) else TRAIN_FLAG_NO_COMPACT
     helper_on = TRAIN_HELPER if helper is None else helper
     if helper_on is not None:

@@ -45,10 +45,16 @@ struct TrainArgs {
   int32_t* err;             // or null: set to 1 by a launch that failed (a flag wait ran out,
                             // fedmx_train_hw.hip); read by elect_wsum_kernel, which then skips
                             // the round's aggregation and adoption (engine/device_round.py)
+  float* vws;               // or null: [k][fedmx_train_av_slot()] workspace of the helper-wave
+                            // kernel's validator workgroups (epoch snapshots, flags); zeroed once
+  uint32_t vseq;            // launch number (> 0, distinct per launch on this workspace): stamps
+                            // the workspace's flags, so no launch reads another's
+  int32_t pad1;
 };
 constexpr int32_t TRAIN_FLAG_NO_COMPACT = 1;  // identity-order kernels even where the compact order applies
 constexpr int32_t TRAIN_FLAG_HELPER = 2;      // helper-wave kernel (fedmx_train_hw.hip) for the compact shapes
 constexpr int32_t TRAIN_FLAG_NO_HELPER = 4;   // never the helper-wave kernel
+constexpr int32_t TRAIN_FLAG_ASYNC_VALID = 16;  // set by the launcher (fedmx_train_hw): validator workgroups
 constexpr int32_t TRAIN_FLAG_TEST_DROP_W4 = 8;   // tests only: one W4 hand-off is never published (a
                                                  // flag-wait timeout in the FedProx helper-wave kernel)
 

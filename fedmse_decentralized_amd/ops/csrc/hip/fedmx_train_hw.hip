@@ -19,11 +19,17 @@
 //     helper reads main w's dY^T / H3^T tiles, forms dW4 (12 MFMAs), runs the
 //     Adam update and publishes W4(s+1) (master rows + A-operand copy).  The
 //     two workgroup barriers of the step are the only synchronisation.
-//   validation: all 8 waves share the epoch's validation batches.
+//   validation: all 8 waves share the epoch's validation batches -- in a
+//     second workgroup per client, the "validator", while the trainer runs
+//     ahead into the next epoch (asynchronous validation, below), or in the
+//     trainer itself at every epoch's end (launches whose 2k workgroups would
+//     not all be resident at once).
 //
 // Barrier sequence (every wave executes exactly this): prologue staging
 // (2 per state tensor), per training step #1 / #2, per epoch: masters
-// published, loss exchange, snapshot; epilogue write-back.
+// published, loss exchange, snapshot (asynchronous: masters published, one
+// decision barrier at step AV_CHECK, the publication; a roll-back: one);
+// epilogue write-back.
 #include "fedmx_train_common.h"
 
 // Timing-only ablations of the main waves' step (WRONG numerics, never a
@@ -141,6 +147,36 @@
 #endif
 constexpr int HW_SPIN_LIMIT = FEDMX_HW_SPIN_LIMIT;
 
+// Asynchronous validation (TRAIN_FLAG_ASYNC_VALID, set by the launcher when
+// TrainArgs.vws is given and 2k workgroups fit the device at once): the
+// epoch-end validation pass (~24,000 cycles of the trainer's 8 waves per epoch,
+// r5 stamps) moves to a second workgroup per client, the "validator", on
+// another CU.  At the end of epoch e the trainer copies its LDS masters and
+// its waves' Adam moments to the workspace, publishes them with an agent-scope
+// release and goes on with epoch e+1 without waiting.  The validator runs the
+// same validation code on the copy (same tiles, waves and fp64 order), writes
+// the valid loss, the best snapshot (save_model) and a stamped decision word
+// (stop or continue, the best epoch).  The trainer reads that word at step
+// AV_CHECK of epoch e+1 (or at its end, for epochs that short): on "stop" it
+// discards the speculative steps -- masters and moments come back from the
+// workspace, the step count from a register -- and leaves as the synchronous
+// kernel would have after epoch e.  Every result (parameters, moments, best
+// snapshot, tracking, epochs run, best epoch) is the synchronous kernel's.
+#ifndef FEDMX_HW_ASYNC_VALID
+#define FEDMX_HW_ASYNC_VALID 1   // instantiation mask (bit 0 plain, bit 1 FedProx, bit 2 batch > 12)
+#endif
+#ifndef FEDMX_HW_AV_CHECK
+#define FEDMX_HW_AV_CHECK 6   // step of epoch e+1 before which the trainer needs epoch e's decision
+#endif
+// wall_clock64() ticks (100 MHz on gfx950) one cross-workgroup wait may take
+// before the launch reports itself failed (an epoch of a large client can
+// take many milliseconds; a validator that never runs must not hang the GPU)
+#ifndef FEDMX_HW_AV_TIMEOUT
+#define FEDMX_HW_AV_TIMEOUT 1000000000LL
+#endif
+constexpr int AV_CHECK = FEDMX_HW_AV_CHECK;
+static_assert(AV_CHECK % 2 == 0, "the ping-pong step loop checks between step pairs");
+
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 // (Round 3 also measured, and removed, seven schedule variants of this step --
 // dH3 partial reads in flight together, the bias column by address select,
@@ -176,6 +212,60 @@ constexpr int L_SCR = 4 * L_T32 + 2 * L_T16;  // 3200 per main wave (dY^T, H3^T,
 constexpr int L_Q4 = 4 * 4 * 64 * 4;     // 4096 W4 rows in the dH3 A-operand layout [w][v][t][lane][4]
 constexpr int L_TOTAL = L_W1 + L_W4 + L_W2 + L_W3 + 3 * L_RED + 4 * L_SCR + L_Q4 + 128;
 static_assert(L_TOTAL * 4 <= 160 * 1024, "LDS budget");
+
+// asynchronous validation workspace of one client slot (floats): the LDS
+// masters region [sW1 | sW4 | sW2 | sW3] as it is (padded strides, bias
+// units), then the flags (ready: u64 at 0, the epoch's FedProx term: f64 at 2,
+// decision: u64 at 32, its own 128-byte line), then every thread's Adam
+// moments (mains: M, V slabs, 40 floats; helpers: M4, V4, 32)
+constexpr int AV_L_M = L_W1 + L_W4 + L_W2 + L_W3;   // 10048
+constexpr int AV_FLAGS = 64;
+constexpr int AV_R = 512 * 40;
+constexpr int AV_SLOT = AV_L_M + AV_FLAGS + AV_R;
+static_assert(AV_L_M % 4 == 0 && AV_SLOT % 64 == 0, "workspace alignment");
+constexpr unsigned AV_FAIL = 0xffffffffu;   // decision word (low half) of a validator whose wait ran out
+// The hand-offs follow the write-through recipe (cdna_hip_programming.md §6
+// Guideline 16, R1 / R2): the snapshot is stored and loaded with sc1
+// (write-through, L1-bypassing) buffer accesses, every storing wave drains
+// its stores (s_waitcnt vmcnt(0)) before the workgroup barrier behind which
+// one lane stores the ready flag; flags and decisions are 8-byte relaxed
+// agent-scope atomics polled relaxed -- no L2 write-back or invalidate
+// (release / acquire fences: ~1.7-6.5 us each) anywhere.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t av_rsrc(float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, AV_L_M * 4, 0x00020000);
+}
+__device__ __forceinline__ void av_store16(__amdgpu_buffer_rsrc_t r, int i, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, i * 16, 0, 16);   // aux 16: sc1
+}
+__device__ __forceinline__ f32x4 av_load16(__amdgpu_buffer_rsrc_t r, int i) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, i * 16, 0, 16));   // sc1
+}
+__device__ __forceinline__ void av_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// flags / decisions / the FedProx term: 8-byte GLOBAL (never flat) agent-scope atomics
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ unsigned long long av_ld(unsigned long long* p) {
+  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void av_st(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// (thread 0 of a trainer) the low half of the decision word `dec` once it is
+// stamped `seq` and covers epoch need - 1, or AV_FAIL when the wait runs out.
+// (Inlined: a call anywhere in the step loop, even on its cold check branch,
+// makes the register allocator spill around it inside the loop.)
+__device__ __forceinline__ unsigned av_wait_decision(unsigned long long* dec, unsigned long long seq, int need) {
+  const long long t0 = (long long)wall_clock64();
+  for (;;) {
+    const unsigned long long d = av_ld(dec);
+    if ((d & 0xffffffff00000000ull) == seq) {
+      const unsigned lo = (unsigned)d;
+      if (lo == AV_FAIL || (int)((lo >> 1) & 0x7fffu) >= need) return lo;
+    }
+    if ((long long)wall_clock64() - t0 > FEDMX_HW_AV_TIMEOUT) return AV_FAIL;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
 
 // main-wave optimizer state: W1 column block (MFMA A-operand layout) + small tile
 struct MSlab {
@@ -252,6 +342,58 @@ __device__ __forceinline__ void lds_to_hslab(HSlab& o, const Lane& L) {
       for (int v = 0; v < 2; ++v) o.q4[v][t][r] = L.w4[(16 * v + r) * S_W4 + 16 * t];
 }
 
+// asynchronous validation: a thread's Adam moments <-> its workspace record
+// (registers as they are: the scaled form of FEDMX_HW_SCALED included)
+__device__ __forceinline__ f32x4 q4v(const float (&a)[4]) { return f32x4{a[0], a[1], a[2], a[3]}; }
+__device__ __forceinline__ void q4set(float (&a)[4], f32x4 v) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) a[r] = v[r];
+}
+__device__ __forceinline__ void mslab_dump(float* rec, const MSlab& M, const MSlab& V) {
+  f32x4* q = reinterpret_cast<f32x4*>(rec);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      q[2 * t + v] = q4v(M.q1[t][v]);
+      q[5 + 2 * t + v] = q4v(V.q1[t][v]);
+    }
+  q[4] = q4v(M.o);
+  q[9] = q4v(V.o);
+}
+__device__ __forceinline__ void mslab_restore(const float* rec, MSlab& M, MSlab& V) {
+  const f32x4* q = reinterpret_cast<const f32x4*>(rec);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      q4set(M.q1[t][v], q[2 * t + v]);
+      q4set(V.q1[t][v], q[5 + 2 * t + v]);
+    }
+  q4set(M.o, q[4]);
+  q4set(V.o, q[9]);
+}
+__device__ __forceinline__ void hslab_dump(float* rec, const HSlab& M, const HSlab& V) {
+  f32x4* q = reinterpret_cast<f32x4*>(rec);
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      q[2 * v + t] = q4v(M.q4[v][t]);
+      q[4 + 2 * v + t] = q4v(V.q4[v][t]);
+    }
+}
+__device__ __forceinline__ void hslab_restore(const float* rec, HSlab& M, HSlab& V) {
+  const f32x4* q = reinterpret_cast<const f32x4*>(rec);
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      q4set(M.q4[v][t], q[2 * v + t]);
+      q4set(V.q4[v][t], q[4 + 2 * v + t]);
+    }
+}
+
 // compact-order product over the two halves of the hidden axis (7 k-steps).
 // SPLIT (FEDMX_SPLIT_CHAINS, per instantiation; fedmx_train.hip the same
 // order): each half in its own accumulator, interleaved, then added -- a
@@ -307,6 +449,15 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   constexpr bool VMASK = (FEDMX_HW_VALUE_MASKS & ROLE) != 0;
   constexpr bool PPONG = (FEDMX_HW_PINGPONG & ROLE) != 0;
   constexpr bool SPLIT = (FEDMX_SPLIT_CHAINS & ROLE) != 0;
+  // asynchronous validation needs barrier #2 to be a workgroup barrier; it is
+  // a mask over the instantiations like the switches above (FedProx and
+  // batch > 12: their step loops spill registers with it compiled in)
+  constexpr bool AVOK = (FEDMX_HW_ASYNC_VALID & ROLE) != 0 && HWF < 2;
+  const bool av_launch = (A.flags & TRAIN_FLAG_ASYNC_VALID) != 0;   // grid: k trainers, then k validators
+  const int nk = av_launch ? (int)gridDim.x / 2 : (int)gridDim.x;
+  if (av_launch && !AVOK && (int)blockIdx.x >= nk) return;
+  const bool av = AVOK && av_launch;
+  const bool validator = av && (int)blockIdx.x >= nk;
   __shared__ __attribute__((aligned(16))) float lds[L_TOTAL];
   const int w8 = threadIdx.x >> 6;
   const bool helper = w8 >= 4;
@@ -389,7 +540,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   const float* const sm_b = w < 2 ? sZT + tr : sH1T + tr + 16 * (w - 2) * S_T;
   float* const redw = sRedDH3 + (w * 2) * 256 + lane * 4;
 
-  const int kslot = blockIdx.x;
+  const int kslot = validator ? (int)blockIdx.x - nk : (int)blockIdx.x;
   const int cid = A.client_idx[kslot];
   float* const Pg = A.params + (size_t)cid * P_PAD;
   float* const Mg = A.adam_m + (size_t)cid * P_PAD;
@@ -695,6 +846,144 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     HSTAMP(ep == 0, 13);
     return worse >= A.patience && worse > 0;
   };
+
+  // ---- asynchronous validation (FEDMX_HW_ASYNC_VALID, see the top of the file)
+  // (the workspace addresses are formed where they are used, from the kernel
+  // arguments: nothing of this stays live through the step loop, whose
+  // FedProx and batch > 12 instantiations sit at the register limit)
+  auto av_ws = [&]() -> float* { return A.vws + (size_t)kslot * AV_SLOT; };
+  auto av_ready = [&]() { return reinterpret_cast<unsigned long long*>(av_ws() + AV_L_M); };
+  auto av_px = [&]() { return reinterpret_cast<unsigned long long*>(av_ws() + AV_L_M + 2); };
+  auto av_dec = [&]() { return reinterpret_cast<unsigned long long*>(av_ws() + AV_L_M + 32); };
+  auto av_rec = [&]() { return av_ws() + AV_L_M + AV_FLAGS + 40 * threadIdx.x; };
+  auto av_seq = [&]() { return (unsigned long long)A.vseq << 32; };
+  bool av_break = false;   // the validator stopped the client: roll back to the last published epoch
+  // (thread 0) the decision word's low half once it covers epoch need - 1, or AV_FAIL
+  auto av_wait_dec = [&](int need) -> unsigned {
+    if (spin_fail) return AV_FAIL;   // (one wait that ran out ends the launch's waiting)
+    const unsigned lo = av_wait_decision(av_dec(), av_seq(), need);
+    if (lo == AV_FAIL) spin_fail = true;
+    return lo;
+  };
+  auto av_stop = [](unsigned lo) { return lo != AV_FAIL && (lo & 1u) != 0; };
+  // trainer, both roles, one workgroup barrier: epoch ep-1's decision
+  // (thread 0 waits for it); true = stop
+  auto av_check = [&](int ep) -> bool {
+    HSTAMP(ep == 1, 20);
+    if (threadIdx.x == 0) sFlag[16] = (int)av_wait_dec(ep);
+    __syncthreads();
+    HSTAMP(ep == 1, 21);
+    return av_stop((unsigned)sFlag[16]);
+  };
+  // trainer, end of epoch ep, both roles: the masters of epoch ep complete in
+  // LDS; an epoch shorter than AV_CHECK steps reads epoch ep-1's decision
+  // here.  True: it said stop -- roll back instead of publishing.
+  auto av_epoch_begin = [&](int ep) -> bool {
+    HSTAMP(ep == 0, 18);
+    __syncthreads();
+    return ep > 0 && nsteps <= AV_CHECK && av_check(ep);
+  };
+  // ... then publish epoch ep: LDS masters -> workspace, train loss, FedProx
+  // term, ready flag (the role then writes its own moments to av_rec, which
+  // only the same thread reads back, after a roll-back)
+  auto av_epoch_publish = [&](int ep, double acc_tr, double prox_now) {
+    const __amdgpu_buffer_rsrc_t rs = av_rsrc(av_ws());
+    for (int i = threadIdx.x; i < AV_L_M / 4; i += 512) av_store16(rs, i, lds_read4(lds + 4 * i));
+    const double s0 = wave_sum_d(acc_tr);
+    const double s2 = wave_sum_d(prox_now);
+    if (lane == 0) {
+      sLoss[w8 * 4 + 0] = s0;
+      sLoss[w8 * 4 + 2] = s2;
+    }
+    av_drain();   // every storing wave, before the barrier behind which lane 0 signals
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double tr_sum = 0.0, px_sum = 0.0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        tr_sum += sLoss[i * 4 + 0];
+        px_sum += sLoss[i * 4 + 2];
+      }
+      A.tracking[((size_t)kslot * A.epochs + ep) * 2] = nb > 0 ? tr_sum / nb : __builtin_nan("");
+      av_st(av_px(), __builtin_bit_cast(unsigned long long, px_sum));
+      av_drain();
+      av_st(av_ready(), av_seq() | (unsigned)(ep + 1));
+    }
+    HSTAMP(ep == 0, 19);
+    ep_run = ep + 1;
+  };
+  // trainer, both roles: the masters of the last published epoch back into
+  // LDS (the role restores its moments from av_rec after this; this thread's
+  // own stores of them are ordered before its loads)
+  auto av_rollback_lds = [&]() {
+    const __amdgpu_buffer_rsrc_t rs = av_rsrc(av_ws());
+    for (int i = threadIdx.x; i < AV_L_M / 4; i += 512) lds_write4(lds + 4 * i, av_load16(rs, i));
+    __syncthreads();
+  };
+
+  // ============================= validator =====================================
+  // (the synchronous epoch_tail's validation, loss order, patience rule and
+  // best snapshot, on the trainer's published copy of each epoch)
+  if (validator) {
+    double min_v = __builtin_huge_val();
+    int worse_v = 0, best_v = -1;
+    for (int ep = 0; ep < A.epochs; ++ep) {
+      if (threadIdx.x == 0) {
+        const unsigned long long want = av_seq() | (unsigned)(ep + 1);
+        const long long t0 = (long long)wall_clock64();
+        int ok = 1;
+        while (av_ld(av_ready()) != want) {
+          if ((long long)wall_clock64() - t0 > FEDMX_HW_AV_TIMEOUT) {
+            ok = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        sFlag[16] = ok;
+        // (the polling lane loads after its poll matched; sc1, like every load of the hand-off)
+        sLoss[3] = ok ? __builtin_bit_cast(double, av_ld(av_px())) : 0.0;
+      }
+      __syncthreads();
+      if (!sFlag[16]) {   // the trainer never published: its launch reports itself failed
+        if (threadIdx.x == 0)
+          av_st(av_dec(), av_seq() | AV_FAIL);
+        return;
+      }
+      {
+        const __amdgpu_buffer_rsrc_t rs = av_rsrc(av_ws());
+        for (int i = threadIdx.x; i < AV_L_M / 4; i += 512) lds_write4(lds + 4 * i, av_load16(rs, i));
+      }
+      __syncthreads();
+      double acc_va = 0.0;
+      for (int vt = w8; vt < nvt; vt += 8) valid_chunk(Xva, 16 * vt, n_va, acc_va);
+      const double s1 = wave_sum_d(acc_va);
+      if (lane == 0) sLoss[w8 * 4 + 1] = s1;
+      __syncthreads();
+      double va_sum = 0.0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) va_sum += sLoss[i * 4 + 1];
+      double valid_loss = nvb > 0 ? va_sum / nvb : __builtin_nan("");
+      if (PROX) valid_loss += (double)A.mu * sLoss[3];
+      if (threadIdx.x == 0) A.tracking[((size_t)kslot * A.epochs + ep) * 2 + 1] = valid_loss;
+      const bool better = valid_loss < min_v;
+      if (better) {
+        min_v = valid_loss;
+        best_v = ep;
+        worse_v = 0;
+      } else {
+        ++worse_v;
+      }
+      const bool stop = worse_v >= A.patience && worse_v > 0;
+      // the decision first (the trainer waits for nothing else), then the best
+      // snapshot from this workgroup's LDS copy, which the trainer never touches
+      if (threadIdx.x == 0)
+        av_st(av_dec(), av_seq() | ((unsigned)(best_v + 1) << 16) | ((unsigned)(ep + 1) << 1) | (stop ? 1u : 0u));
+      if (better && stager) masters_to_global_o<CP, BU>(Bg, sW1, sW4, sW2, sW3);  // save_model(): best snapshot
+      if (stop) return;
+      __syncthreads();   // masters and sLoss read before the next epoch's copy
+    }
+    return;
+  }
   // prologue staging: the stagers issue the loads of every state tensor
   // (m, v, [anchor], params) in one memory round trip, then each tensor
   // passes through the masters in turn (the barrier sequence of one global_to_masters_o pass per tensor)
@@ -770,6 +1059,11 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       int mb = 0, mch = 0;   // MULTI: batch / chunk of this step
       f32x4 G4[2][2];
       for (int bi = 0; bi < nsteps; ++bi) {
+        // (asynchronous validation: the mains' check before step AV_CHECK)
+        if (AVOK && av && ep > 0 && bi == AV_CHECK && av_check(ep)) {
+          av_break = true;
+          break;
+        }
         const bool hs = (ep == 0 && bi == STAMP_STEP);
         const int nch = MULTI ? (min(B, n_tr - mb * B) + 15) / 16 : 1;
         const bool first_ch = !MULTI || mch == 0;
@@ -861,7 +1155,18 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
             }
         prox_now = (double)pr;
       }
-      if (epoch_tail(ep, acc_tr, prox_now)) break;
+      if (av) {
+        if (av_break || av_epoch_begin(ep)) {   // stopped after epoch ep-1: discard epoch ep
+          av_break = true;
+          av_rollback_lds();
+          hslab_restore(av_rec(), M4, V4);
+          break;
+        }
+        av_epoch_publish(ep, acc_tr, prox_now);
+        hslab_dump(av_rec(), M4, V4);   // (own roll-back record: after the publication, undrained)
+      } else if (epoch_tail(ep, acc_tr, prox_now)) {
+        break;
+      }
     }
     // write back (barriers as the main branch; the mains stage to global)
     if (FEDMX_HW_SCALED) {
@@ -887,6 +1192,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 
   // ============================= main waves =====================================
   int js = 0;   // step index within the launch (selects the Adam-scalar slot)
+  int step_e = step;   // asynchronous validation: the Adam step count of the last published epoch
   MSlab P, M, V, AN;
   stage_vals(pv_m);
   lds_to_mslab(M, L);
@@ -1276,15 +1582,30 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       __builtin_amdgcn_iglp_opt(FEDMX_HW_IGLP);
 #endif
     };
+    // (asynchronous validation: the decision on epoch ep-1 before step
+    // AV_CHECK, an even step, so the chunk buffers keep their roles)
     if constexpr (PPONG) {
       int bi = 0;
       for (; bi + 1 < nsteps; bi += 2) {
+        if (AVOK && av && ep > 0 && bi == AV_CHECK && av_check(ep)) {
+          av_break = true;
+          break;
+        }
         train_step(bi, cur, nxt);
         train_step(bi + 1, nxt, cur);
       }
-      if (bi < nsteps) train_step(bi, cur, nxt);
+      if (bi < nsteps && !av_break) {
+        if (AVOK && av && ep > 0 && bi == AV_CHECK && av_check(ep))   // (an epoch of AV_CHECK + 1 steps)
+          av_break = true;
+        else
+          train_step(bi, cur, nxt);
+      }
     } else {
       for (int bi = 0; bi < nsteps; ++bi) {
+        if (AVOK && av && ep > 0 && bi == AV_CHECK && av_check(ep)) {
+          av_break = true;
+          break;
+        }
         train_step(bi, cur, nxt);
         cur = nxt;
       }
@@ -1309,7 +1630,20 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
       prox_now = (double)pr;
     }
-    if (epoch_tail(ep, acc_tr, prox_now)) break;
+    if (av) {
+      if (av_break || av_epoch_begin(ep)) {   // stopped after epoch ep-1: discard epoch ep
+        av_break = true;
+        av_rollback_lds();
+        mslab_restore(av_rec(), M, V);
+        step = step_e;
+        break;
+      }
+      av_epoch_publish(ep, acc_tr, prox_now);
+      mslab_dump(av_rec(), M, V);   // (own roll-back record: after the publication, undrained)
+      step_e = step;
+    } else if (epoch_tail(ep, acc_tr, prox_now)) {
+      break;
+    }
   }
 
   // ---- write back: params (masters), then m and v through the same staging
@@ -1334,10 +1668,20 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   HSTAMP(true, 31);
   if (threadIdx.x == 0) {
     // a flag wait of any wave ran out: the launch's results are invalid
-    const bool failed = *(volatile int*)sFail != 0;
+    bool failed = *(volatile int*)sFail != 0;
+    int best = best_ep;
+    if (av && ep_run > 0) {
+      // the validator's word on the last epoch kept (after a roll-back: the
+      // stop decision itself); its best epoch
+      const unsigned lo = av_break ? (unsigned)sFlag[16] : av_wait_dec(ep_run);
+      if (lo == AV_FAIL)
+        failed = true;
+      else
+        best = (int)(lo >> 16) - 1;
+    }
     A.adam_step[cid] = step;
     A.epochs_run[kslot] = failed ? -1000 : ep_run;
-    A.best_epoch[kslot] = best_ep;
+    A.best_epoch[kslot] = best;
     if (failed && A.err != nullptr) *A.err = 1;
   }
 }
@@ -1347,27 +1691,54 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 
 extern "C" {
 
+static int g_last_grid = 0;   // workgroups of the last helper-wave launch (tests: 2k = validators ran)
+int fedmx_train_hw_last_grid(void) { return g_last_grid; }
+
 // Helper-wave training launch for the compact reference shapes; returns -4
 // when the shapes need the general kernel (fedmx_train).
 int fedmx_train_hw(const void* args, int k, hipStream_t stream) {
   if (k <= 0) return 0;
-  const fedmx::TrainArgs& A = *reinterpret_cast<const fedmx::TrainArgs*>(args);
+  fedmx::TrainArgs A = *reinterpret_cast<const fedmx::TrainArgs*>(args);
   if (!(A.batch >= 1 && A.d_in >= 1 && A.d_in <= fedmx::DP - 1 && A.hidden >= 1 && A.hidden <= 27 &&
         A.latent >= 1 && A.latent <= 7))
     return -4;
   const bool multi = A.batch > 12;   // 16-row chunks per batch
+  // asynchronous validation: one validator workgroup per client beside the
+  // trainers, only when all 2k workgroups (one per CU: 132 KB of LDS each)
+  // can be resident at once -- a trainer waits for its validator's decisions
+  int grid = k;
+  A.flags &= ~fedmx::TRAIN_FLAG_ASYNC_VALID;
+  const int hwf = multi ? 0 : (A.mu != 0.f ? FEDMX_HW_FLAGS_PROX : FEDMX_HW_FLAGS);   // the kernel's HWF
+  const int role = multi ? 4 : (A.mu != 0.f ? 2 : 1);                                 // the kernel's ROLE
+  if ((FEDMX_HW_ASYNC_VALID & role) && A.vws != nullptr && A.vseq != 0 && A.epochs >= 1 && hwf < 2) {
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = -1;
+    }
+    if (2 * k <= cus) {
+      A.flags |= fedmx::TRAIN_FLAG_ASYNC_VALID;
+      grid = 2 * k;
+    }
+  }
+  g_last_grid = grid;
   if (A.mu != 0.f) {
     if (multi)
-      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true, true>), dim3(k), dim3(512), 0, stream, A);
+      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true, true>), dim3(grid), dim3(512), 0, stream, A);
     else
-      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true, false>), dim3(k), dim3(512), 0, stream, A);
+      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true, false>), dim3(grid), dim3(512), 0, stream, A);
   } else {
     if (multi)
-      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<false, true>), dim3(k), dim3(512), 0, stream, A);
+      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<false, true>), dim3(grid), dim3(512), 0, stream, A);
     else
-      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<false, false>), dim3(k), dim3(512), 0, stream, A);
+      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<false, false>), dim3(grid), dim3(512), 0, stream, A);
   }
   return (int)hipGetLastError();
 }
+
+// floats of one client slot of TrainArgs.vws
+int fedmx_train_av_slot(void) { return fedmx::hw::AV_SLOT; }
 
 }  // extern "C"

@@ -51,7 +51,11 @@ VARIANTS = {
     "sepadam": ["-DFEDMX_ADAM_FMA=0"],            # separately rounded Adam    (+3%)
     "dw4late": ["-DFEDMX_DW4_LATE=1"],            # dW4 products after barrier #2 (+0.5%)
     "split_chains": ["-DFEDMX_SPLIT_CHAINS=7"],   # L2 / dZ as two accumulator chains everywhere (r5h: plain -0.7 %, b64 -0.3 %, FedProx +1.2 %: production mask 5)
-    "nosplit": ["-DFEDMX_SPLIT_CHAINS=0"],
+    "nosplit": ["-DFEDMX_SPLIT_CHAINS=0"],        # one accumulator chain everywhere (the r5g build)
+    "noav": ["-DFEDMX_HW_ASYNC_VALID=0"],         # epoch-end validation inside the trainer workgroup (synchronous)
+    "avc4": ["-DFEDMX_HW_AV_CHECK=4"],            # the trainer needs epoch e's decision before step 4 of e+1
+    "avc8": ["-DFEDMX_HW_AV_CHECK=8"],            # ... before step 8
+    "avc40": ["-DFEDMX_HW_AV_CHECK=40"],          # ... before step 40 (never waits: the fixed cost of the path)
     "novgprform": ["-mllvm", "-amdgpu-mfma-vgpr-form=0"],  # AGPR accumulators (+3.3%)
     "noslp": ["-fno-slp-vectorize"],              # no packed fp32 VALU        (+5%)
     "w4pos1": ["-DFEDMX_W4_POS=1"],               # W4 Adam after dH1, fenced   (+2.5%)

@@ -54,6 +54,8 @@ PHASES_HW = [
     (8, 10, "helper: adam W4"), (10, 11, "helper: publish W4 + scalars"),
     (16, 17, "valid: one 16-row tile (one wave)"), (14, 15, "valid: epoch pass (per wave)"),
     (12, 13, "epoch tail (barriers, validation, exchange, snapshot)"),
+    (18, 19, "async validation: epoch-0 end (snapshot, moments, publish)"),
+    (20, 21, "async validation: epoch-1 decision check (step AV_CHECK)"),
     (28, 29, "prologue (state load, mains)"), (30, 31, "epilogue (write back, mains)"),
 ]
 FOUR = "--four-waves" in sys.argv
