@@ -195,9 +195,19 @@ namespace hw {
     if ((cond) && A.stamps != nullptr && blockIdx.x == 0 && lane == 0)                          \
       A.stamps[w8 * 32 + (i)] = __builtin_amdgcn_s_memtime();                                  \
   } while (0)
+// asynchronous-validation timeline of client slot 0 (trainer and validator,
+// wave 0 lane 0): wall_clock64() ticks (one clock for every CU)
+#define AVSTAMP(cond, i)                                                                     \
+  do {                                                                                       \
+    if ((cond) && A.stamps != nullptr && kslot == 0 && threadIdx.x == 0)                     \
+      A.stamps[(i)] = (uint64_t)wall_clock64();                                              \
+  } while (0)
 #else
 #define HSTAMP(cond, i) \
   do {                  \
+  } while (0)
+#define AVSTAMP(cond, i) \
+  do {                   \
   } while (0)
 #endif
 
@@ -870,7 +880,9 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // (thread 0 waits for it); true = stop
   auto av_check = [&](int ep) -> bool {
     HSTAMP(ep == 1, 20);
+    AVSTAMP(ep == 2, 23);   // trainer: epoch 1's decision needed
     if (threadIdx.x == 0) sFlag[16] = (int)av_wait_dec(ep);
+    AVSTAMP(ep == 2, 24);   // trainer: ... received
     __syncthreads();
     HSTAMP(ep == 1, 21);
     return av_stop((unsigned)sFlag[16]);
@@ -905,9 +917,13 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         px_sum += sLoss[i * 4 + 2];
       }
       A.tracking[((size_t)kslot * A.epochs + ep) * 2] = nb > 0 ? tr_sum / nb : __builtin_nan("");
+      // (the FedProx term, 0 without FedProx, and a drain before the flag in
+      // every instantiation: without them the plain launch measured 12 us
+      // slower, r5z -- the flag then queues behind the waves' moment records)
       av_st(av_px(), __builtin_bit_cast(unsigned long long, px_sum));
       av_drain();
       av_st(av_ready(), av_seq() | (unsigned)(ep + 1));
+      AVSTAMP(ep == 1, 22);   // trainer: epoch 1 published
     }
     HSTAMP(ep == 0, 19);
     ep_run = ep + 1;
@@ -940,6 +956,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           __builtin_amdgcn_s_sleep(2);
         }
         sFlag[16] = ok;
+        AVSTAMP(ep == 1, 25);   // validator: epoch 1 seen
         // (the polling lane loads after its poll matched; sc1, like every load of the hand-off)
         sLoss[3] = ok ? __builtin_bit_cast(double, av_ld(av_px())) : 0.0;
       }
@@ -959,6 +976,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       const double s1 = wave_sum_d(acc_va);
       if (lane == 0) sLoss[w8 * 4 + 1] = s1;
       __syncthreads();
+      AVSTAMP(ep == 1, 26);   // validator: validation pass done
       double va_sum = 0.0;
 #pragma unroll
       for (int i = 0; i < 8; ++i) va_sum += sLoss[i * 4 + 1];
@@ -978,6 +996,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       // snapshot from this workgroup's LDS copy, which the trainer never touches
       if (threadIdx.x == 0)
         av_st(av_dec(), av_seq() | ((unsigned)(best_v + 1) << 16) | ((unsigned)(ep + 1) << 1) | (stop ? 1u : 0u));
+      AVSTAMP(ep == 1, 27);   // validator: decision stored
       if (better && stager) masters_to_global_o<CP, BU>(Bg, sW1, sW4, sW2, sW3);  // save_model(): best snapshot
       if (stop) return;
       __syncthreads();   // masters and sLoss read before the next epoch's copy
@@ -1163,7 +1182,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           break;
         }
         av_epoch_publish(ep, acc_tr, prox_now);
-        hslab_dump(av_rec(), M4, V4);   // (own roll-back record: after the publication, undrained)
+        if (ep + 1 < A.epochs) hslab_dump(av_rec(), M4, V4);   // (own roll-back record: after the publication, undrained)
       } else if (epoch_tail(ep, acc_tr, prox_now)) {
         break;
       }
@@ -1639,7 +1658,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         break;
       }
       av_epoch_publish(ep, acc_tr, prox_now);
-      mslab_dump(av_rec(), M, V);   // (own roll-back record: after the publication, undrained)
+      if (ep + 1 < A.epochs) mslab_dump(av_rec(), M, V);   // (own roll-back record: after the publication, undrained)
       step_e = step;
     } else if (epoch_tail(ep, acc_tr, prox_now)) {
       break;

@@ -56,7 +56,6 @@ VARIANTS = {
     "avc4": ["-DFEDMX_HW_AV_CHECK=4"],            # the trainer needs epoch e's decision before step 4 of e+1
     "avc8": ["-DFEDMX_HW_AV_CHECK=8"],            # ... before step 8
     "avc40": ["-DFEDMX_HW_AV_CHECK=40"],          # ... before step 40 (never waits: the fixed cost of the path)
-    "avc4": ["-DFEDMX_HW_AV_CHECK=4"],            # ... before step 4
     "avc2": ["-DFEDMX_HW_AV_CHECK=2"],            # ... before step 2
     "av3": ["-DFEDMX_HW_ASYNC_VALID=3"],          # asynchronous validation for FedProx too
     "av7": ["-DFEDMX_HW_ASYNC_VALID=7"],          # ... and for batch > 12

@@ -90,11 +90,23 @@ def main():
         res = {}
         for a, b, name in phases:
             res[name] = [int(st[w, b] - st[w, a]) if st[w, a] and st[w, b] else None for w in range(nw)]
+        if helper and not FOUR:
+            # asynchronous validation, client 0: wall_clock64 ticks (100 MHz) in slots 22..27
+            raw = stamps.cpu().numpy().astype(np.int64)
+            names = {22: "trainer: epoch 1 published", 25: "validator: epoch 1 seen",
+                     26: "validator: validation done", 27: "validator: decision stored",
+                     23: "trainer: decision needed (step AV_CHECK)", 24: "trainer: decision received"}
+            if raw[22]:
+                res["async validation timeline (us after epoch 1 published)"] = {
+                    v: round((int(raw[i]) - int(raw[22])) / 100.0, 2) for i, v in names.items() if raw[i]}
         out[f"rep{rep}"] = res
         stamps.zero_()
     last = out[f"rep{len(out) - 1}"]
     print(f"{'phase (ticks, rep ' + str(len(out) - 1) + ')':52s} " + " ".join(f"{'w' + str(w):>6s}" for w in range(nw)))
     for name, v in last.items():
+        if isinstance(v, dict):
+            print(name + ": " + ", ".join(f"{k} {x}" for k, x in v.items()))
+            continue
         print(f"{name:52s} " + " ".join(f"{x:6d}" if x is not None else "     -" for x in v))
     if "--json" in sys.argv:
         with open(sys.argv[sys.argv.index("--json") + 1], "w") as f:
