@@ -151,9 +151,10 @@ constexpr int HW_SPIN_LIMIT = FEDMX_HW_SPIN_LIMIT;
 // TrainArgs.vws is given and 2k workgroups fit the device at once): the
 // epoch-end validation pass (~24,000 cycles of the trainer's 8 waves per epoch,
 // r5 stamps) moves to a second workgroup per client, the "validator", on
-// another CU.  At the end of epoch e the trainer copies its LDS masters and
-// its waves' Adam moments to the workspace, publishes them with an agent-scope
-// release and goes on with epoch e+1 without waiting.  The validator runs the
+// another CU.  At the end of epoch e the trainer copies its LDS masters to
+// the workspace (write-through stores, drained, then one flag: no fences),
+// keeps its waves' Adam moments in a per-thread record of its own and goes on
+// with epoch e+1 without waiting.  The validator runs the
 // same validation code on the copy (same tiles, waves and fp64 order), writes
 // the valid loss, the best snapshot (save_model) and a stamped decision word
 // (stop or continue, the best epoch).  The trainer reads that word at step
@@ -161,7 +162,11 @@ constexpr int HW_SPIN_LIMIT = FEDMX_HW_SPIN_LIMIT;
 // discards the speculative steps -- masters and moments come back from the
 // workspace, the step count from a register -- and leaves as the synchronous
 // kernel would have after epoch e.  Every result (parameters, moments, best
-// snapshot, tracking, epochs run, best epoch) is the synchronous kernel's.
+// snapshot, tracking, epochs run, best epoch) is the synchronous kernel's
+// (tests/test_async_validation_gpu.py).  Measured (profiles/r5_train_kernel_ab.md):
+// plain launch 874 -> 842 us, bench +3.5 %, paper configuration +4.6 %; the
+// FedProx and batch > 12 instantiations measured slower and keep the
+// synchronous epoch tail.
 #ifndef FEDMX_HW_ASYNC_VALID
 #define FEDMX_HW_ASYNC_VALID 1   // instantiation mask (bit 0 plain, bit 1 FedProx, bit 2 batch > 12)
 #endif
