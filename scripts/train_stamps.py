@@ -71,7 +71,8 @@ def main():
     eng = HipEngine(DEFAULT_DIMS, dev)
     eng.setup([c.train for c in clients], [c.valid for c in clients], [c.test for c in clients],
               [c.test_label for c in clients], init)
-    hp = TrainHParams(epochs=5, batch_size=12, lr=1e-3, shrink_lambda=5.0, patience=10 ** 6)
+    mu = float(sys.argv[sys.argv.index("--mu") + 1]) if "--mu" in sys.argv else 0.0   # FedProx instantiation
+    hp = TrainHParams(epochs=5, batch_size=12, lr=1e-3, shrink_lambda=5.0, patience=10 ** 6, fedprox_mu=mu)
     stamps = torch.zeros(8 * 32, dtype=torch.int64, device=dev)
     helper = not FOUR
     nw = 8 if helper else 4
