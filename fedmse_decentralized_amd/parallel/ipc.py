@@ -231,6 +231,7 @@ class IpcComm(TorchDistComm):
         n = min(self._gather.slot_words, 4 * 4096 + 12)
         n -= n % 4
         ok = True
+        bad = []   # which checks failed on this rank (logged: the agreement only says who)
         for it in range(3):
             src = (torch.arange(n, device=dev, dtype=torch.float32) * (it + 1) + 1000.0 * me)
             out = torch.full((W, n), -1.0, device=dev, dtype=torch.float32)
@@ -238,7 +239,10 @@ class IpcComm(TorchDistComm):
             exp = torch.stack([torch.arange(n, device=dev, dtype=torch.float32) * (it + 1) + 1000.0 * r
                                for r in range(W)])
             torch.cuda.synchronize(dev)
-            ok &= bool(torch.equal(out, exp))
+            if not torch.equal(out, exp):
+                ok = False
+                wrong = (out != exp).any(dim=1).nonzero().flatten().tolist()
+                bad.append(f"gather {it}: rows from ranks {wrong}")
         m = min(64, self._reduce.slot_words // (2 * W))   # doubles per rank block
         for it in range(2 if m >= 1 else 0):
             t = torch.zeros(W * m, device=dev, dtype=torch.float64)
@@ -246,8 +250,15 @@ class IpcComm(TorchDistComm):
             self._reduce.reduce_f64(t, stream)
             exp = torch.cat([torch.arange(m, device=dev, dtype=torch.float64) + 0.5 * it + r for r in range(W)])
             torch.cuda.synchronize(dev)
-            ok &= bool(torch.equal(t, exp))
-        ok &= self.status_ok()
+            if not torch.equal(t, exp):
+                ok = False
+                bad.append(f"reduce {it}")
+        if not self.status_ok():
+            ok = False
+            bad.append("a wait timed out")
+        if bad:
+            log.warning("rank %d: peer-memory self-test (slot %d words, n %d): %s", self.rank,
+                        self._gather.slot_words, n, "; ".join(bad))
         return ok
 
     def status_ok(self) -> bool:
