@@ -60,6 +60,7 @@ VARIANTS = {
     "avc2": ["-DFEDMX_HW_AV_CHECK=2"],            # ... before step 2
     "av3": ["-DFEDMX_HW_ASYNC_VALID=3"],          # asynchronous validation for FedProx too
     "av7": ["-DFEDMX_HW_ASYNC_VALID=7"],          # ... and for batch > 12
+    "stamps_avc4": ["-DFEDMX_STAMPS=1", "-DFEDMX_HW_AV_CHECK=4"],   # timeline of the step-4 check (scripts/train_stamps.py --lib)
     "novgprform": ["-mllvm", "-amdgpu-mfma-vgpr-form=0"],  # AGPR accumulators (+3.3%)
     "noslp": ["-fno-slp-vectorize"],              # no packed fp32 VALU        (+5%)
     "w4pos1": ["-DFEDMX_W4_POS=1"],               # W4 Adam after dH1, fenced   (+2.5%)
