@@ -38,6 +38,7 @@ VARIANTS = {
     # r4: per-epoch Adam-scalar table (ktab): +1.0 %, removed (commit 96da3e2)
     # r4: dH3 partial reads four at a time per tile, fenced (red4): +10.1 %, removed
     # r5: per-wave dZ partials exchanged at barrier #2 (dzp): plain +12 %, removed
+    # r5: forward kernels' first row tile loaded before the parameter staging: no gain, removed
     "noiglp": ["-DFEDMX_HW_IGLP=-1"],               # r4: no iglp_opt hint in the step loop
     "iglp1": ["-DFEDMX_HW_IGLP=1"],                 # r4: iglp_opt(1) in the step loop
     "flags2": ["-DFEDMX_HW_FLAGS=2"],                # r4: no workgroup barrier in the step loop
