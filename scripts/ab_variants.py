@@ -39,6 +39,10 @@ VARIANTS = {
     # r4: dH3 partial reads four at a time per tile, fenced (red4): +10.1 %, removed
     # r5: per-wave dZ partials exchanged at barrier #2 (dzp): plain +12 %, removed
     # r5: forward kernels' first row tile loaded before the parameter staging: no gain, removed
+    # r5 (r5sch): LLVM scheduler strategies for the whole library (-mllvm -amdgpu-sched-strategy=max-ilp /
+    #   iterative-minreg / max-memory-clause, -amdgpu-use-amdgpu-trackers, -misched-postra-direction=bottomup,
+    #   -amdgpu-disable-unclustered-high-rp-reschedule; iterative-ilp crashes the compiler): plain train launch
+    #   864 / 932 / 922 / 865 / 892 / 845 us vs 842-846 default -- none faster, removed
     "noiglp": ["-DFEDMX_HW_IGLP=-1"],               # r4: no iglp_opt hint in the step loop
     "iglp1": ["-DFEDMX_HW_IGLP=1"],                 # r4: iglp_opt(1) in the step loop
     "flags2": ["-DFEDMX_HW_FLAGS=2"],                # r4: no workgroup barrier in the step loop
