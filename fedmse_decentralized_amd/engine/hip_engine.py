@@ -3,14 +3,20 @@
 * ``train_launch``  -> ``fedmx_train`` (persistent fused local training, one
                        workgroup per client, all selected clients in one launch;
                        results stay on the device until the next ``fetch``)
+                       -- the reference's per-client epoch loop with Adam,
+                       validation and patience, src/Trainer/client_trainer.py:360-419
 * ``forward_rows``  -> ``fedmx_forward_rows`` (any list of model x row-block pairs)
 * ``vote_scores``   -> ``fedmx_standardize_lds`` + ``fedmx_forward_rows`` +
                        ``fedmx_score_reduce`` (3 launches, no host sync)
+                       -- src/Trainer/client_trainer.py:220-238 (standardised
+                       voter data, batches of 128)
 * ``verify_stats``  -> ``fedmx_forward_rows`` + ``fedmx_score_reduce`` + ``fedmx_param_drift``
+                       -- src/Trainer/model_verifier.py:79-99
 * ``adopt``         -> ``fedmx_broadcast_rows``
 * ``evaluate``      -> cached plans: ``fedmx_forward_rows`` (latents / SSE of every
                        hosted client) + ``fedmx_cen_score`` + ``fedmx_auc``
-* ``weighted_sum``  -> ``fedmx_weighted_sum``
+                       -- src/Evaluator/evaluator.py:56-94
+* ``weighted_sum``  -> ``fedmx_weighted_sum`` -- src/Trainer/client_trainer.py:107-130
 
 Descriptor arrays are cached on the device for static work and streamed
 through a pinned ring otherwise; device->host traffic goes through a pinned

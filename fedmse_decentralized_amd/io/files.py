@@ -10,6 +10,11 @@ when the content got shorter — ``model.cpt`` has a fixed size for fixed
 model dims), an append one ``write`` on an ``O_APPEND`` descriptor (~3 us
 each).  The bytes on disk are exactly what ``open(..., "wb"/"a")`` would
 leave.  Not thread-safe: owned by the single writer thread.
+
+(The artefacts themselves are the reference's: ``model.cpt`` from
+``save_model``, src/Trainer/client_trainer.py:340-345, and
+``training_tracking.pkl``, :405-419, which the reference re-creates with
+``open(..., "wb")`` on every write.)
 """
 from __future__ import annotations
 
