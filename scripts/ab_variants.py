@@ -60,7 +60,7 @@ VARIANTS = {
     "nosplit": ["-DFEDMX_SPLIT_CHAINS=0"],        # one accumulator chain everywhere (the r5g build)
     "noav": ["-DFEDMX_HW_ASYNC_VALID=0"],         # epoch-end validation inside the trainer workgroup (synchronous)
     "avc4": ["-DFEDMX_HW_AV_CHECK=4"],            # the trainer needs epoch e's decision before step 4 of e+1
-    "avc8": ["-DFEDMX_HW_AV_CHECK=8"],            # ... before step 8
+    "avc8": ["-DFEDMX_HW_AV_CHECK=8"],            # ... before step 8 (r5avc: 844 / 844 us vs 843 / 845, also 10 / 12: same)
     "avc40": ["-DFEDMX_HW_AV_CHECK=40"],          # ... before step 40 (never waits: the fixed cost of the path)
     "avc2": ["-DFEDMX_HW_AV_CHECK=2"],            # ... before step 2
     "av3": ["-DFEDMX_HW_ASYNC_VALID=3"],          # asynchronous validation for FedProx too
