@@ -357,7 +357,8 @@ class DeviceRound:
     def _check_failed(self, rec: dict) -> None:
         if int(rec["report"][0]) == _hip.ELECT_TRAIN_FAILED:
             raise RuntimeError(f"round {rec['round'] + 1}: a training launch failed (a wave's bounded flag wait "
-                               "ran out); the device skipped that round's aggregation and adoption")
+                               "or validator decision wait ran out); the device skipped that round's aggregation "
+                               "and adoption")
 
     def enqueue(self, selected: List[int]) -> LazyRoundResult:
         fed = self.fed

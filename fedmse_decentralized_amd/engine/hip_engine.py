@@ -81,9 +81,10 @@ class HipEngine(Engine):
         tr, er, be = host
         er = er.astype(np.int64)
         if bool(np.any(er < 0)):
-            # fedmx_train_hw.hip: an LDS flag hand-off ran out its bounded wait
+            # fedmx_train_hw.hip: an LDS flag hand-off or a trainer's wait for its
+            # validator workgroup's decision ran out its bounded wait
             raise RuntimeError(f"fused training kernel failed (epochs_run {er.tolist()}): a wave's flag wait "
-                               "timed out; results of this launch are invalid")
+                               "or a validator decision wait timed out; results of this launch are invalid")
         track = [[(float(tr[i, e, 0]), float(tr[i, e, 1])) for e in range(int(er[i]))]
                  for i in range(len(handle.local_ids))]
         return TrainResult(handle.local_ids, er, track, be.astype(np.int64))

@@ -36,6 +36,7 @@ TRAIN_FLAG_NO_COMPACT = 1
 TRAIN_FLAG_HELPER = 2
 TRAIN_FLAG_NO_HELPER = 4
 TRAIN_FLAG_TEST_DROP_W4 = 8   # tests only: inject a flag-wait timeout (fedmx_train_hw.hip)
+TRAIN_FLAG_TEST_MUTE_VALIDATOR = 32   # tests only: client slot 0's validator never answers (0.2 s timeout)
 # extra TrainArgs.flags bits OR'd into every launch (tests/test_train_failure_gpu.py)
 TRAIN_TEST_FLAGS = 0
 # helper-wave training kernel (fedmx_train_hw.hip: 8 waves, W4's gradient and
@@ -707,6 +708,23 @@ def standardize_ddof1(x: torch.Tensor, d_in: int, out: Optional[torch.Tensor] = 
     return y
 
 
+def ranks_share_device(environ=None, device_count=None) -> bool:
+    """True when several ranks of this job run on one GPU (one-box
+    rehearsals: ``FEDMX_DEVICE_INDEX`` pins every rank to one device, or
+    torchrun started more local ranks than there are devices).  Their
+    training launches then compete for the CUs, so a trainer's validator
+    workgroup is no longer guaranteed to be resident beside it: those launches
+    keep the synchronous epoch tail."""
+    env = os.environ if environ is None else environ
+    world = int(env.get("LOCAL_WORLD_SIZE", env.get("WORLD_SIZE", "1")))
+    if world <= 1:
+        return False
+    if "FEDMX_DEVICE_INDEX" in env:
+        return True
+    n = torch.cuda.device_count() if device_count is None else device_count
+    return world > n
+
+
 class TrainBuffers:
     """Persistent per-store device buffers for the training launch."""
 
@@ -737,7 +755,9 @@ class TrainBuffers:
         earlier launches never match."""
         if self.vws is None:
             cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
-            self.vslots = max(0, min(int(n_rows), cus // 2))
+            # one trainer + one validator CU per client, and this process alone
+            # on the device (no validator when ranks share it)
+            self.vslots = 0 if ranks_share_device() else max(0, min(int(n_rows), cus // 2))
             self.vws = torch.zeros(max(self.vslots, 1) * int(lib().fedmx_train_av_slot()), dtype=torch.float32,
                                    device=self.dev)
         if k > self.vslots:

@@ -152,12 +152,69 @@ def build_hip(force: bool = False, verbose: bool = False, extra_flags=(), target
     # -amdgpu-mfma-vgpr-form: MFMA accumulators in arch VGPRs (the training
     # kernel otherwise pays ~150 v_accvgpr moves per step on its VALU-bound
     # optimizer tail: -3.3% launch time measured)
-    flags = [f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-             "-ffp-contract=off", "-munsafe-fp-atomics", "-mllvm", "-amdgpu-mfma-vgpr-form=1", *extra_flags]
+    base = _hip_flags(extra_flags)
+    flags = [*base[:3], "-fPIC", "-shared", *base[3:]]
     digest = content_hash([compiler_identity(hipcc_path()), *flags, *(p.name for p in srcs)], srcs + _headers())
     return _build(target, digest,
                   lambda tmp: [hipcc_path(), *flags, f"-I{CSRC / 'hip'}", *map(str, srcs), "-o", str(tmp)],
                   force, verbose)
+
+
+def _hip_flags(extra_flags=()):
+    return [f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-munsafe-fp-atomics",
+            "-mllvm", "-amdgpu-mfma-vgpr-form=1", *extra_flags]
+
+
+def kernel_resources(source: str = "fedmx_train_hw.hip", extra_flags=(), asm: bool = False) -> dict:
+    """Per-kernel register / spill / scratch figures of one HIP source as the
+    library's flags compile it for the GPU (hipcc ``-Rpass-analysis=
+    kernel-resource-usage``; no GPU needed).  Returns ``{mangled name: {"vgpr",
+    "agpr", "sgpr", "vgpr_spill", "sgpr_spill", "scratch", "lds", "occupancy"}}``;
+    with ``asm=True`` also ``{"__asm__": the device assembly}``."""
+    import re
+    import tempfile
+
+    src = CSRC / "hip" / source
+    keys = {"VGPRs": "vgpr", "AGPRs": "agpr", "TotalSGPRs": "sgpr", "VGPRs Spill": "vgpr_spill",
+            "SGPRs Spill": "sgpr_spill", "ScratchSize [bytes/lane]": "scratch", "LDS Size [bytes/block]": "lds",
+            "Occupancy [waves/SIMD]": "occupancy"}
+    with tempfile.TemporaryDirectory() as td:
+        out = Path(td) / ("k.s" if asm else "k.o")
+        cmd = [hipcc_path(), *[f for f in _hip_flags(extra_flags) if f not in ("-fPIC",)], "--cuda-device-only",
+               "-S" if asm else "-c", f"-I{CSRC / 'hip'}", str(src), "-o", str(out),
+               "-Rpass-analysis=kernel-resource-usage"]
+        log = _run(cmd)
+        res: dict = {}
+        cur = None
+        for line in log.splitlines():
+            m = re.search(r"remark:\s+(.*?) \[-Rpass-analysis", line)
+            if not m:
+                continue
+            text = m.group(1)
+            if text.startswith("Function Name:"):
+                cur = res.setdefault(text.split(":", 1)[1].strip(), {})
+                continue
+            k, _, v = text.rpartition(":")
+            if cur is not None and k.strip() in keys:
+                cur[keys[k.strip()]] = int(v.strip())
+        if asm:
+            res["__asm__"] = out.read_text()
+    return res
+
+
+def train_resource_report(extra_flags=()) -> str:
+    """One line per helper-wave training instantiation: VGPRs, spills, scratch."""
+    names = {"_ZN5fedmx2hw15train_kernel_hwILb0ELb0EEEvNS_9TrainArgsE": "plain (batch <= 12)",
+             "_ZN5fedmx2hw15train_kernel_hwILb1ELb0EEEvNS_9TrainArgsE": "FedProx (batch <= 12)",
+             "_ZN5fedmx2hw15train_kernel_hwILb0ELb1EEEvNS_9TrainArgsE": "plain, batch > 12",
+             "_ZN5fedmx2hw15train_kernel_hwILb1ELb1EEEvNS_9TrainArgsE": "FedProx, batch > 12"}
+    res = kernel_resources("fedmx_train_hw.hip", extra_flags)
+    rows = ["instantiation            VGPR  VGPR-spill  SGPR-spill  scratch B/lane  LDS B"]
+    for k, label in names.items():
+        r = res.get(k, {})
+        rows.append(f"{label:24s} {r.get('vgpr', '?'):>4}  {r.get('vgpr_spill', '?'):>10}  {r.get('sgpr_spill', '?'):>10}"
+                    f"  {r.get('scratch', '?'):>14}  {r.get('lds', '?'):>5}")
+    return "\n".join(rows)
 
 
 def build_all(force: bool = False, verbose: bool = False):
@@ -176,6 +233,9 @@ def describe(target: Path) -> str:
 
 
 if __name__ == "__main__":
+    if "--resources" in sys.argv:   # register / spill / scratch report of the training kernel
+        print(train_resource_report())
+        sys.exit(0)
     force = "--force" in sys.argv
     for p in build_all(force=force, verbose=True):
         print(describe(p))

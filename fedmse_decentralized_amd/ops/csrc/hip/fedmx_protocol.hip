@@ -500,12 +500,9 @@ struct VerifyArgs {
 };
 static_assert(sizeof(VerifyArgs) == sizeof(DecideArgs) + 48, "VerifyArgs layout is shared with Python");
 
-// FEDMX_VERIFY_ABLATE (timing-only builds, wrong results; scripts/r2_verify_ablate.sh
-// after `python scripts/ab_variants.py build vabl1 vabl2 vabl4`): 1 no forward,
-// 2 no drift, 4 no adoption / snapshot pass
-#ifndef FEDMX_VERIFY_ABLATE
-#define FEDMX_VERIFY_ABLATE 0
-#endif
+// (r2 timing-only ablations of this kernel -- no forward 13.4 us, no drift
+// 18.9 us, no adoption pass 21.4 us, of 24.6 us -- are in git history and
+// profiles/r2_verify_ablations.md)
 // REL: the relative drift limit (mode 3) is compiled in only where it is used
 template <bool CP, bool REL>
 __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) {
@@ -526,7 +523,7 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     // of client blockIdx.x - n_local (independent of every decision, so it
     // runs beside the verification instead of in its adoption pass)
     const int cl2 = blockIdx.x - A.n_local;
-    if (cl2 >= A.n_local || (FEDMX_VERIFY_ABLATE & 4)) return;
+    if (cl2 >= A.n_local) return;
     const size_t o2 = (size_t)cl2 * A.P;
     const f32x4* b = reinterpret_cast<const f32x4*>(V.best + o2);
     f32x4* bs = reinterpret_cast<f32x4*>(V.best_stage + o2);
@@ -560,7 +557,7 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     d.d_in = A.d_in;
     d.latent = V.latent;
     d.hidden = V.hidden;
-    if (!(FEDMX_VERIFY_ABLATE & 1)) {
+    {
       stage_params<CP>(A.agg, sW1, sW2, sW3, sW4);
       __syncthreads();
       fwd_rows_block<CP>(d, sW1, sW2, sW3, sW4, wv, 8, s_sse);
@@ -598,7 +595,7 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     // instead of one per 4 elements (6 dependent rounds, ~5 us of the kernel).
     float drift = 0.f, hnorm = 0.f;
     const bool rel = REL && A.mode == 3;
-    if (had_hist && (A.mode == 0 || rel) && !(FEDMX_VERIFY_ABLATE & 2)) {
+    if (had_hist && (A.mode == 0 || rel)) {
       const float* h = A.hist + off;
       constexpr int NJ = (P_PAD + 1023) / 1024;
       int sg[2][NJ];
@@ -686,7 +683,6 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
     load = ok;
   }
   // ---- adoption + history + snapshots in one pass over the row
-  if (FEDMX_VERIFY_ABLATE & 4) return;
   // (ModelVerifier receivers, absolute or relative drift limit: the history
   // becomes the received aggregate whatever the decision)
   const bool receiver = a >= 0 && c != a && (A.mode == 0 || A.mode == 3);

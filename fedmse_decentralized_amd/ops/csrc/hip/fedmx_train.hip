@@ -40,45 +40,13 @@
 // columns and padded features are masked out of the loss and every gradient.
 #include "fedmx_train_common.h"
 
-// 0: compiler schedule; 1..3: sched_group_barrier MFMA/VALU interleaving
-// patterns; 4: iglp_opt(0) (fastest measured with the compact order and the
-// FMA-form Adam: 1.211 vs 1.231 ms compiler / 1.257 ms pattern 1 per
-// 5-client x 5-epoch launch); 5: iglp_opt(1)
-#ifndef FEDMX_DW4_LATE
-#define FEDMX_DW4_LATE 0
-#endif
-#ifndef FEDMX_SCHED_HINTS
-#define FEDMX_SCHED_HINTS 4
-#endif
-// Timing-only ablations (scripts/ab_variants.py "abl_*"; WRONG numerics, never
-// a production build): drop one piece of the step to measure what it costs
-// on the step's critical path.  1 = skip W4's gradient + Adam, 2 = skip W1's
-// Adam, 4 = skip the small tiles' Adam, 8 = skip every Adam update.
-#ifndef FEDMX_ABLATE
-#define FEDMX_ABLATE 0
-#endif
-// placement of W4's Adam update in the step (see w4_update); measured
-// (r2, 5 clients x 5 epochs): 0 1.090 ms, 1 1.117 ms, 2 1.112 ms
-#ifndef FEDMX_W4_POS
-#define FEDMX_W4_POS 0
-#endif
-// 1: scaled-moment Adam (adam4s, fedmx_train_common.h: 7 instead of 10 VALU
-// issues per parameter); 0: adam4.  Measured (r2): 1.096 vs 1.091 ms here --
-// this kernel's step is bound by its dependent chain -- but the helper-wave
-// kernel (fedmx_train_hw.hip) is SIMD-issue bound and gains 3 % with it (r5),
-// so both use it by default (the two kernels stay bit-identical: the shared
-// adam_scaled_step / adam_moment_in_scale); the IEEE-Adam build does not.
-#ifndef FEDMX_ADAM_SCALED
-#define FEDMX_ADAM_SCALED (!FEDMX_EXACT_ADAM)
-#endif
-#if FEDMX_ADAM_SCALED && FEDMX_EXACT_ADAM
-#error "FEDMX_ADAM_SCALED rounds differently from torch; the IEEE-Adam build needs FEDMX_ADAM_SCALED=0"
-#endif
-#if FEDMX_ADAM_SCALED
-#define FEDMX_ADAM4 adam4s
-#else
-#define FEDMX_ADAM4 adam4
-#endif
+// (Rounds 1-5 measured, and removed, these variants of this kernel's step:
+// sched_group_barrier MFMA/VALU interleavings (+9 %) and the compiler's own
+// schedule (+2.5 %) against iglp_opt(0); dW4's products after barrier #2
+// (+0.5 %); W4's Adam after dH1 or after the next layer-1 issue (+2.5 / +2 %);
+// separately rounded Adam (+3 %); the timing-only ablations that located the
+// optimizer's share of the step.  Source in git history, numbers in
+// scripts/ab_variants.py and profiles/r2_*.)
 
 namespace fedmx {
 
@@ -183,13 +151,11 @@ __device__ __forceinline__ void scale_slab(Slab& o, float f) {
 // (k-steps (t, s)): L2 (W2a H1) and dZ (W3a^T dH3).  These are the dependent
 // chains on the step's critical path (one accumulator: 7-8 x 40-cycle MFMA
 // latency); SPLIT sums each half in its own accumulator and adds the two, so
-// the chain is ~half as long.  FEDMX_SPLIT_CHAINS is a mask over the
-// instantiations (bit 0 plain, bit 1 FedProx), defined with
-// fedmx_train_hw.hip's (whose bit 2, batch > 12, has no instantiation of its
-// own here) so that the two kernels sum in the same order.
-#ifndef FEDMX_SPLIT_CHAINS
-#define FEDMX_SPLIT_CHAINS 5
-#endif
+// the chain is ~half as long.  SPLIT_CHAINS is a mask over the
+// instantiations (bit 0 plain, bit 1 FedProx, bit 2 batch > 12), shared with
+// fedmx_train_hw.hip (whose bit 2 has no instantiation here) so that the two
+// kernels sum in the same order.  r5h A/B: plain -0.7 %, batch 64 -0.3 %,
+// FedProx +1.2 % with split chains (profiles/r5_train_kernel_ab.md).
 template <bool CP, bool SPLIT>
 __device__ __forceinline__ f32x4 chain2(f32x4 a0, f32x4 a1, f32x4 b0, f32x4 b1) {
   f32x4 x = zero4();
@@ -233,7 +199,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   static_assert(ONE || !CP, "compact order needs single-tile batches");
   constexpr int KB = CP ? 3 : 4;   // k-steps of products over the batch
   constexpr int KZ = CP ? 2 : 4;   // k-steps of products over the latent axis
-  constexpr bool SPLIT = (FEDMX_SPLIT_CHAINS & (PROX ? 2 : 1)) != 0;
+  constexpr bool SPLIT = (SPLIT_CHAINS & (PROX ? 2 : 1)) != 0;
   __shared__ __attribute__((aligned(16))) float lds[L_TOTAL];
   const int w = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -293,7 +259,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   __syncthreads();
   // moment scales of the scaled-moment Adam (identity otherwise)
   const float c1 = 1.f - A.beta1, c2 = 1.f - A.beta2;
-  if (FEDMX_ADAM_SCALED) {
+  if (ADAM_SCALED) {
     scale_slab(M, adam_moment_in_scale(A.beta1));
     scale_slab(V, adam_moment_in_scale(A.beta2));
   }
@@ -677,13 +643,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         // 1 - beta ** step), computed at the batch start, off the critical path
         b1pow *= (double)A.beta1;
         b2pow *= (double)A.beta2;
-        if (FEDMX_ADAM_SCALED) {
-          adam_scaled_step(K, KI, b1pow, b2pow);
-        } else {
-          K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
-          K.bc2s = (float)sqrt(1.0 - b2pow);
-          K.inv_bc2s = 1.0f / K.bc2s;
-        }
+        adam_step_scalars(K, KI, A.lr, b1pow, b2pow);
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -749,28 +709,22 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       STAMP(stamp_on, 4);
       wave_sync();
       // ---- dW4 (own rows) accumulated over the batch's chunks.  Operands are
-      // read here (sT0 is reused for dH3^T below); with FEDMX_DW4_LATE the
-      // products are issued after barrier #2, off the path to the barrier,
-      // where they fill the MFMA gaps of the dependent dZ / dH1 chains.
+      // read here (sT0 is reused for dH3^T below).
       const f32x4 w4a0 = lds_read4(sT0 + tr);
       const f32x4 w4a1 = lds_read4(sT0 + tr + 16 * S_T);
       const f32x4 w4b0 = lds_read4(sT1 + tr);
       const f32x4 w4b1 = lds_read4(sT1 + tr + 16 * S_T);
-      auto dw4_products = [&]() {
 #pragma unroll
-        for (int s = 0; s < KB; ++s) {
-          G4[0][0] = mfma16(w4a0[s], w4b0[s], G4[0][0]);
-          G4[0][1] = mfma16(w4a0[s], w4b1[s], G4[0][1]);
-          G4[1][0] = mfma16(w4a1[s], w4b0[s], G4[1][0]);
-          G4[1][1] = mfma16(w4a1[s], w4b1[s], G4[1][1]);
-        }
-      };
-      if (!FEDMX_DW4_LATE) dw4_products();
+      for (int s = 0; s < KB; ++s) {
+        G4[0][0] = mfma16(w4a0[s], w4b0[s], G4[0][0]);
+        G4[0][1] = mfma16(w4a0[s], w4b1[s], G4[0][1]);
+        G4[1][0] = mfma16(w4a1[s], w4b0[s], G4[1][0]);
+        G4[1][1] = mfma16(w4a1[s], w4b1[s], G4[1][1]);
+      }
       STAMP(stamp_on, 5);
       STAMP(stamp_on, 6);
       __syncthreads();  // barrier #2: dH3 partials of all waves visible
       STAMP(stamp_on, 7);
-      if (FEDMX_DW4_LATE) dw4_products();
       f32x4 dh3[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -790,24 +744,16 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       float prox_acc = 0.f;  // sum (p - anchor)^2 of owned params (pre-update)
       // W4's Adam update + publish (its rows are read back by this wave only,
       // by the next layer-4 product).  W4 is not read again this step (its
-      // dH3 product ran before barrier #2).  FEDMX_W4_POS places it (ONE
-      // kernels): 0 here, where its VALU work is meant to overlap the
-      // backward MFMAs; 1 after the dH1 product, 2 after the next chunk's
-      // layer-1 issue — both behind a scheduling fence, so the dependent
-      // dZ -> dH1 -> dW1 chain is issued first.
-      auto w4_update = [&]() {
-        if (FEDMX_ABLATE & 9) return;
+      // dH3 product ran before barrier #2); here its VALU work overlaps the
+      // backward MFMAs.
+      if (last) {
+        ++step;
 #pragma unroll
         for (int v = 0; v < 2; ++v)
 #pragma unroll
           for (int t = 0; t < 2; ++t)
-            FEDMX_ADAM4<PROX>(P.q4[v][t], M.q4[v][t], V.q4[v][t], AN.q4[v][t], G4[v][t], K, prox_acc);
+            adam_update<PROX>(P.q4[v][t], M.q4[v][t], V.q4[v][t], AN.q4[v][t], G4[v][t], K, prox_acc);
         w4_to_lds(P, L);
-      };
-      constexpr int W4POS = ONE ? FEDMX_W4_POS : 0;
-      if (last) {
-        ++step;
-        if (W4POS == 0) w4_update();
       }
       // dH3^T for the owned dW3 tile (dY^T reads are done).  Written by every
       // wave (own scratch) so the step stays one basic block for the scheduler.
@@ -840,11 +786,6 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
         dh1b[t] = acc;
       }
       STAMP(stamp_on, 8);
-      if (W4POS == 1) {
-        __builtin_amdgcn_sched_barrier(0);
-        w4_update();
-        __builtin_amdgcn_sched_barrier(0);
-      }
       // ---- dW1^T (own columns) = X^T dH1: D[d=4g+r][h=c] lands in the q1 layout
 #pragma unroll
       for (int s = 0; s < KB; ++s) {
@@ -866,57 +807,26 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
       STAMP(stamp_on, 9);
       if (last) {
         // W1 first: the next chunk's layer-1 product waits on it
-        if (!(FEDMX_ABLATE & 10)) {
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int v = 0; v < 2; ++v)
-              FEDMX_ADAM4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
-        }
+          for (int v = 0; v < 2; ++v)
+            adam_update<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
         STAMP(stamp_on, 10);
         // (after an epoch's last batch this works on a stale tile; the result
         // is unused and the product stays branch-free)
         finalize_chunk(bc_n, nxt);
         l1_partial(nxt, l1a, l1b);
-        if (W4POS == 2) {
-          __builtin_amdgcn_sched_barrier(0);
-          w4_update();
-        }
-        if (!(FEDMX_ABLATE & 12)) FEDMX_ADAM4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
+        adam_update<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
         if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
         // publish the owned small tile (read by every wave after barrier #1)
         own_to_lds(P, L);
-#if FEDMX_SCHED_HINTS
-        if (ONE) {
-          // Everything from barrier #2 to here is one basic block (ONE): ask
-          // the scheduler to interleave the optimizer / mask VALU work into
-          // the MFMA gaps (one wave per SIMD co-issues ~6 VALU per 16x16x4
-          // MFMA) instead of running the two streams back to back.
-#if FEDMX_SCHED_HINTS == 1
-#pragma unroll
-          for (int i = 0; i < 64; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // 6 VALU
-          }
-#elif FEDMX_SCHED_HINTS == 2
-#pragma unroll
-          for (int i = 0; i < 48; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-          }
-#elif FEDMX_SCHED_HINTS == 3
-#pragma unroll
-          for (int i = 0; i < 48; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);
-          }
-#elif FEDMX_SCHED_HINTS == 4
-          __builtin_amdgcn_iglp_opt(0);
-#elif FEDMX_SCHED_HINTS == 5
-          __builtin_amdgcn_iglp_opt(1);
-#endif
-        }
-#endif
+        // Everything from barrier #2 to here is one basic block (ONE): the
+        // scheduler interleaves the optimizer / mask VALU work into the MFMA
+        // gaps (one wave per SIMD co-issues ~6 VALU per 16x16x4 MFMA) instead
+        // of running the two streams back to back (iglp_opt(0): 1.211 vs
+        // 1.231 ms with the compiler's schedule per 5-client x 5-epoch launch)
+        if (ONE) __builtin_amdgcn_iglp_opt(0);
       } else {
         finalize_chunk(bc_n, nxt);
         l1_partial(nxt, l1a, l1b);
@@ -1014,7 +924,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const TrainArgs A) {
   __syncthreads();
   masters_to_global_o<CP>(Pg, sW1, sW4, sW2, sW3);
   __syncthreads();
-  if (FEDMX_ADAM_SCALED) {
+  if (ADAM_SCALED) {
     scale_slab(M, c1);
     scale_slab(V, c2);
   }
@@ -1039,13 +949,10 @@ extern "C" {
 
 int fedmx_train_hw(const void* args, int k, hipStream_t stream);  // fedmx_train_hw.hip
 
-// 1: the compact shapes train on the helper-wave kernel unless the caller
-// asks otherwise (TRAIN_FLAG_NO_HELPER); 0: only when asked (TRAIN_FLAG_HELPER).
-// Measured (r2, 5 clients x 5 epochs): 1.058 vs 1.090 ms, FedProx 1.137 vs
-// 1.231 ms; bit-identical parameters (tests/test_kernels_gpu.py).
-#ifndef FEDMX_TRAIN_HW_DEFAULT
-#define FEDMX_TRAIN_HW_DEFAULT 1
-#endif
+// The compact shapes train on the helper-wave kernel unless the caller asks
+// otherwise (TRAIN_FLAG_NO_HELPER).  Measured (r2, 5 clients x 5 epochs):
+// 1.058 vs 1.090 ms, FedProx 1.137 vs 1.231 ms; bit-identical parameters
+// (tests/test_kernels_gpu.py).
 
 int fedmx_train(const void* args, int k, hipStream_t stream) {
   if (k <= 0) return 0;
@@ -1060,8 +967,7 @@ int fedmx_train(const void* args, int k, hipStream_t stream) {
   // batches of <= 12 rows
   const bool cpl = A.hidden <= 27 && A.latent <= 7 && !(A.flags & fedmx::TRAIN_FLAG_NO_COMPACT);
   const bool cp = A.batch <= 12 && cpl;
-  const bool hw = cpl && !(A.flags & fedmx::TRAIN_FLAG_NO_HELPER) &&
-                  (FEDMX_TRAIN_HW_DEFAULT || (A.flags & fedmx::TRAIN_FLAG_HELPER));
+  const bool hw = cpl && !(A.flags & fedmx::TRAIN_FLAG_NO_HELPER);
   if (hw) return fedmx_train_hw(args, k, stream);
   if (A.mu != 0.f) {
     if (cp)

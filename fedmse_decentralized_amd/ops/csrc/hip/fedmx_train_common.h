@@ -4,20 +4,18 @@
 #pragma once
 #include "fedmx_common.h"
 
-// 1: IEEE square root and divisions in the Adam denominator / quotient
-// (adam4) instead of the hardware v_sqrt_f32 / v_rcp_f32
+// Build variants of the training kernels (the only two compile-time switches
+// of the training sources besides the launch-time tunables of
+// fedmx_train_hw.hip; every other variant measured in rounds 1-5 lives in git
+// history and in profiles/r*_train_*):
+//   FEDMX_EXACT_ADAM=1  torch's exact Adam rounding sequence (IEEE square root
+//                       and divisions: adam4) instead of the scaled-moment
+//                       form (adam4s); libfedmx_hip_exact.so, the long-horizon
+//                       parity test
+//   FEDMX_STAMPS=1      in-kernel s_memtime phase stamps (libfedmx_hip_stamps.so,
+//                       scripts/train_stamps.py)
 #ifndef FEDMX_EXACT_ADAM
 #define FEDMX_EXACT_ADAM 0
-#endif
-// 1: fused multiply-adds in the Adam update where torch's CPU vector kernels
-// fuse (lerp, addcmul, addcdiv; also fewer VALU issues on the optimizer-bound
-// tail of the step, -2% launch time measured); 0: every multiply and add
-// separately rounded
-#ifndef FEDMX_ADAM_FMA
-#define FEDMX_ADAM_FMA 1
-#endif
-#if FEDMX_EXACT_ADAM && !FEDMX_ADAM_FMA
-#error "FEDMX_EXACT_ADAM follows torch's fused lerp/addcmul: it needs FEDMX_ADAM_FMA=1"
 #endif
 
 namespace fedmx {
@@ -57,6 +55,8 @@ constexpr int32_t TRAIN_FLAG_NO_HELPER = 4;   // never the helper-wave kernel
 constexpr int32_t TRAIN_FLAG_ASYNC_VALID = 16;  // set by the launcher (fedmx_train_hw): validator workgroups
 constexpr int32_t TRAIN_FLAG_TEST_DROP_W4 = 8;   // tests only: one W4 hand-off is never published (a
                                                  // flag-wait timeout in the FedProx helper-wave kernel)
+constexpr int32_t TRAIN_FLAG_TEST_MUTE_VALIDATOR = 32;   // tests only: client slot 0's validator never answers
+                                                         // (a decision-wait timeout, 0.2 s)
 
 // In-kernel phase timestamps (build with -DFEDMX_STAMPS=1): wave w's lane 0 of
 // workgroup 0 records s_memtime at fixed points of training step STAMP_STEP
@@ -82,7 +82,7 @@ struct AdamStep {
   float b1, kd, ed;   // scaled form (adam4s)
 };
 
-// Scaled-moment Adam (fedmx_train.hip, FEDMX_ADAM_SCALED): the kernel keeps
+// Scaled-moment Adam (both training kernels; not in FEDMX_EXACT_ADAM builds): the kernel keeps
 //   mh = m / (1-b1),  vh = v / (1-b2)
 // in registers for the whole launch (scaled on load, unscaled on write-back),
 // which turns torch's update into
@@ -145,21 +145,17 @@ __device__ __forceinline__ void adam_scaled_step(AdamStep& K, const AdamScaledIn
 // moment scale on load (m / (1-b1), v / (1-b2)); the write-back multiplies by 1-b
 __device__ __forceinline__ float adam_moment_in_scale(float beta) { return (float)(1.0 / (double)(1.f - beta)); }
 
-// torch.optim.Adam single-tensor update (no weight decay / amsgrad):
+// torch.optim.Adam single-tensor update (no weight decay / amsgrad), the
+// FEDMX_EXACT_ADAM build:
 //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2)
 //   p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1)
-// Default build: lerp and addcmul fused as torch's CPU vector kernels fuse
-// them, the denominator and the update as two fused multiply-adds around the
-// hardware square root and reciprocal (<= 1 ulp each): over 5,700 steps at
-// the paper's hyper-parameters it agrees with the torch oracle to 6e-8 in the
-// parameters (tests/test_long_horizon_gpu.py).  FEDMX_EXACT_ADAM=1: torch's
-// exact rounding sequence with IEEE square root and divisions (54 % slower
-// launch, profiles/r4_train_hw_experiments.md).
-// Four elements (one accumulator register quad) at a time, stage-major: every
-// stage issues four independent scalar ops, so consecutive VALU instructions
-// never depend on each other (no hazard s_nops between dependent packed ops,
-// which the packed-fp32 form paid on gfx950) and the scheduler can slot them
-// into MFMA gaps.
+// torch's CPU op sequence, rounding for rounding (checked against torch 2.10
+// on the CPU: lerp and addcmul fused, `(sqrt(v) / bc2s) + eps` and addcdiv's
+// `p + (value * m) / denom` separately rounded); only torch's vectorised sqrt
+// (SLEEF, 0.5001 ulp: ~0.6 % of inputs off by one ulp) differs from the IEEE
+// square root used here (54 % slower launch than adam4s,
+// profiles/r4_train_hw_experiments.md; tests/test_long_horizon_gpu.py).
+// Four elements (one accumulator register quad) at a time, stage-major.
 template <bool PROX>
 __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4], const float (&a)[4], f32x4 g,
                                       const AdamStep& K, float& prox_acc) {
@@ -174,10 +170,6 @@ __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4
 #pragma unroll
     for (int r = 0; r < 4; ++r) gr[r] = gr[r] + K.two_mu * t0[r];
   }
-#if FEDMX_ADAM_FMA
-  // fused multiply-adds where the torch op sequence has a multiply feeding
-  // an add (lerp, addcmul, the denominator and addcdiv): one rounding
-  // instead of two per pair, 10 instead of 14 VALU issues per parameter.
 #pragma unroll
   for (int r = 0; r < 4; ++r) t0[r] = gr[r] - m[r];
 #pragma unroll
@@ -188,12 +180,6 @@ __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4
   for (int r = 0; r < 4; ++r) t1[r] = K.one_m_b2 * gr[r];
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(t1[r], gr[r], t0[r]);
-#if FEDMX_EXACT_ADAM
-  // torch's CPU op sequence, rounding for rounding (checked against torch
-  // 2.10 on the CPU: lerp and addcmul fused, `(sqrt(v) / bc2s) + eps` and
-  // addcdiv's `p + (value * m) / denom` separately rounded); only torch's
-  // vectorised sqrt (SLEEF, 0.5001 ulp: ~0.6 % of inputs off by one ulp)
-  // differs from the IEEE square root used here
 #pragma unroll
   for (int r = 0; r < 4; ++r) t0[r] = __fsqrt_rn(v[r]);
 #pragma unroll
@@ -204,117 +190,35 @@ __device__ __forceinline__ void adam4(float (&p)[4], float (&m)[4], float (&v)[4
   for (int r = 0; r < 4; ++r) t1[r] = t1[r] / t0[r];
 #pragma unroll
   for (int r = 0; r < 4; ++r) p[r] = p[r] + t1[r];
-#else
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t0[r] = __builtin_amdgcn_sqrtf(v[r]);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t0[r] = __builtin_fmaf(t0[r], K.inv_bc2s, K.eps);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t1[r] = __builtin_amdgcn_rcpf(t0[r]);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t1[r] = m[r] * t1[r];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) p[r] = __builtin_fmaf(K.neg_step_size, t1[r], p[r]);
-#endif
-#else
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t0[r] = gr[r] - m[r];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) m[r] = m[r] + K.one_m_b1 * t0[r];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t0[r] = v[r] * K.b2;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t1[r] = (K.one_m_b2 * gr[r]) * gr[r];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = t0[r] + t1[r];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t0[r] = __builtin_amdgcn_sqrtf(v[r]);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t0[r] = t0[r] * K.inv_bc2s + K.eps;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t1[r] = __builtin_amdgcn_rcpf(t0[r]);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) t1[r] = m[r] * t1[r];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) p[r] = p[r] + K.neg_step_size * t1[r];
-#endif
 }
 
-// adam4 (FMA form) on float pairs: every non-transcendental step is one
-// packed-fp32 instruction for two parameters (v_pk_add / v_pk_mul /
-// v_pk_fma_f32: the same per-element IEEE results as the scalar ops, so the
-// update is bit-identical to adam4).  No FedProx term (its loss sum keeps the
-// scalar order).
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void adam4_packed(float (&p)[4], float (&m)[4], float (&v)[4], f32x4 g,
-                                             const AdamStep& K) {
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const f32x2 G = {g[2 * h], g[2 * h + 1]};
-    f32x2 M = {m[2 * h], m[2 * h + 1]};
-    f32x2 V = {v[2 * h], v[2 * h + 1]};
-    f32x2 P = {p[2 * h], p[2 * h + 1]};
-    const f32x2 omb1 = {K.one_m_b1, K.one_m_b1}, b2 = {K.b2, K.b2}, omb2 = {K.one_m_b2, K.one_m_b2};
-    const f32x2 ibc = {K.inv_bc2s, K.inv_bc2s}, eps = {K.eps, K.eps}, ns = {K.neg_step_size, K.neg_step_size};
-    M = __builtin_elementwise_fma(omb1, G - M, M);
-    V = __builtin_elementwise_fma(omb2 * G, G, V * b2);
-    f32x2 d = {__builtin_amdgcn_sqrtf(V.x), __builtin_amdgcn_sqrtf(V.y)};
-    d = __builtin_elementwise_fma(d, ibc, eps);
-    const f32x2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-    P = __builtin_elementwise_fma(ns, M * r, P);
-    m[2 * h] = M.x;
-    m[2 * h + 1] = M.y;
-    v[2 * h] = V.x;
-    v[2 * h + 1] = V.y;
-    p[2 * h] = P.x;
-    p[2 * h + 1] = P.y;
+// L2 / dZ products as two accumulator chains, per instantiation (bit 0
+// plain, bit 1 FedProx, bit 2 batch > 12): chain2 in both training kernels
+constexpr int SPLIT_CHAINS = 5;
+
+// the build's Adam form: scaled moments (moments in registers as m/(1-b1),
+// v/(1-b2) for the whole launch) unless FEDMX_EXACT_ADAM
+constexpr bool ADAM_SCALED = !FEDMX_EXACT_ADAM;
+template <bool PROX>
+__device__ __forceinline__ void adam_update(float (&p)[4], float (&m)[4], float (&v)[4], const float (&a)[4], f32x4 g,
+                                            const AdamStep& K, float& prox_acc) {
+  if constexpr (ADAM_SCALED)
+    adam4s<PROX>(p, m, v, a, g, K, prox_acc);
+  else
+    adam4<PROX>(p, m, v, a, g, K, prox_acc);
+}
+// the per-step scalars of the build's form for the step whose bias
+// corrections are 1 - b1pow, 1 - b2pow
+__device__ __forceinline__ void adam_step_scalars(AdamStep& K, const AdamScaledInit& I, float lr, double b1pow,
+                                                  double b2pow) {
+  if constexpr (ADAM_SCALED) {
+    adam_scaled_step(K, I, b1pow, b2pow);
+  } else {
+    K.neg_step_size = (float)(-((double)lr / (1.0 - b1pow)));
+    K.bc2s = (float)sqrt(1.0 - b2pow);
+    K.inv_bc2s = 1.0f / K.bc2s;
   }
 }
-
-// dense global [P_PAD] <-> LDS masters
-__device__ __forceinline__ void global_to_masters(const float* __restrict__ src, float* sW1, float* sW4,
-                                                  float* sW2, float* sW3) {
-  const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
-  for (int i = threadIdx.x; i < P_PAD / 4; i += blockDim.x) {
-    const f32x4 val = s4[i];
-    int e = i * 4;
-    if (e < OFF_W2) {
-      lds_write4(&sW1[(e / DP) * S_W1 + (e % DP)], val);
-    } else if (e < OFF_W3) {
-      e -= OFF_W2;
-      lds_write4(&sW2[(e / HP) * S_W2 + (e % HP)], val);
-    } else if (e < OFF_W4) {
-      e -= OFF_W3;
-      lds_write4(&sW3[(e / ZP) * S_W3 + (e % ZP)], val);
-    } else {
-      e -= OFF_W4;
-      lds_write4(&sW4[(e / HP) * S_W4 + (e % HP)], val);
-    }
-  }
-}
-
-__device__ __forceinline__ void masters_to_global(float* __restrict__ dst, const float* sW1, const float* sW4,
-                                                  const float* sW2, const float* sW3) {
-  f32x4* d4 = reinterpret_cast<f32x4*>(dst);
-  for (int i = threadIdx.x; i < P_PAD / 4; i += blockDim.x) {
-    int e = i * 4;
-    f32x4 val;
-    if (e < OFF_W2) {
-      val = lds_read4(&sW1[(e / DP) * S_W1 + (e % DP)]);
-    } else if (e < OFF_W3) {
-      e -= OFF_W2;
-      val = lds_read4(&sW2[(e / HP) * S_W2 + (e % HP)]);
-    } else if (e < OFF_W4) {
-      e -= OFF_W3;
-      val = lds_read4(&sW3[(e / ZP) * S_W3 + (e % ZP)]);
-    } else {
-      e -= OFF_W4;
-      val = lds_read4(&sW4[(e / HP) * S_W4 + (e % HP)]);
-    }
-    d4[i] = val;
-  }
-}
-
 
 // ---- compact internal order (train_kernel<.., CP = true>) --------------------
 // For the reference shapes (hidden <= 27, latent <= 7, batch <= 12) the kernel
@@ -369,6 +273,18 @@ __device__ __forceinline__ int batch_row_of_col(int p) {
 constexpr int STAGE_PER_THREAD = P_PAD / 4 / 256;
 static_assert(STAGE_PER_THREAD * 4 * 256 == P_PAD, "staging assumes 256 threads");
 
+// the staging thread index, opaque to the optimiser: every staging pass
+// forms its LDS addresses afresh instead of keeping the ~40 addresses of the
+// first pass live (spilled) across the whole launch for the write-back
+// (only the 256 staging threads call the staging passes: the range keeps
+// their per-element branches resolved at compile time)
+__device__ __forceinline__ int stage_tid() {
+  int t = (int)threadIdx.x;
+  asm volatile("" : "+v"(t));
+  __builtin_assume(t >= 0 && t < 256);
+  return t;
+}
+
 template <bool CP>
 __device__ __forceinline__ float* master_slot(int e, int i, float* sW1, float* sW4, float* sW2, float* sW3) {
   // LDS address of storage element e + i (e a multiple of 4, i in 0..3)
@@ -397,9 +313,10 @@ __device__ __forceinline__ void stage_load(const float* __restrict__ src, f32x4 
 template <bool CP>
 __device__ __forceinline__ void vals_to_masters_o(const f32x4 (&val)[STAGE_PER_THREAD], float* sW1, float* sW4,
                                                   float* sW2, float* sW3) {
+  const int tid = stage_tid();
 #pragma unroll
   for (int k = 0; k < STAGE_PER_THREAD; ++k) {
-    const int e = 4 * (threadIdx.x + 256 * k);
+    const int e = 4 * (tid + 256 * k);
     if (e < OFF_W2 || !CP) {   // rows permuted at most: one float4
       lds_write4(master_slot<CP>(e, 0, sW1, sW4, sW2, sW3), val[k]);
     } else {
@@ -416,9 +333,10 @@ __device__ __forceinline__ void global_to_masters_o(const float* __restrict__ sr
   f32x4 val[STAGE_PER_THREAD];
 #pragma unroll
   for (int k = 0; k < STAGE_PER_THREAD; ++k) val[k] = s4[threadIdx.x + 256 * k];
+  const int tid = stage_tid();
 #pragma unroll
   for (int k = 0; k < STAGE_PER_THREAD; ++k) {
-    const int e = 4 * (threadIdx.x + 256 * k);
+    const int e = 4 * (tid + 256 * k);
     if (e < OFF_W2 || !CP) {   // rows permuted at most: one float4
       lds_write4(master_slot<CP>(e, 0, sW1, sW4, sW2, sW3), val[k]);
     } else {
@@ -429,15 +347,16 @@ __device__ __forceinline__ void global_to_masters_o(const float* __restrict__ sr
 }
 
 // CLEAR_BU: the helper-wave kernel's in-launch bias units (the last element
-// of W1, W2, W3 and W4, fedmx_train_hw.hip FEDMX_HW_BIAS_UNITS) are written as 0
+// of W1, W2, W3 and W4, fedmx_train_hw.hip, "bias units") are written as 0
 template <bool CP, bool CLEAR_BU = false>
 __device__ __forceinline__ void masters_to_global_o(float* __restrict__ dst, float* sW1, float* sW4, float* sW2,
                                                     float* sW3) {
   f32x4* d4 = reinterpret_cast<f32x4*>(dst);
   f32x4 val[STAGE_PER_THREAD];
+  const int tid = stage_tid();
 #pragma unroll
   for (int k = 0; k < STAGE_PER_THREAD; ++k) {
-    const int e = 4 * (threadIdx.x + 256 * k);
+    const int e = 4 * (tid + 256 * k);
     if (e < OFF_W2 || !CP) {
       val[k] = lds_read4(master_slot<CP>(e, 0, sW1, sW4, sW2, sW3));
     } else {
@@ -449,7 +368,7 @@ __device__ __forceinline__ void masters_to_global_o(float* __restrict__ dst, flo
       val[k][3] = 0.f;
   }
 #pragma unroll
-  for (int k = 0; k < STAGE_PER_THREAD; ++k) d4[threadIdx.x + 256 * k] = val[k];
+  for (int k = 0; k < STAGE_PER_THREAD; ++k) d4[tid + 256 * k] = val[k];
 }
 
 }  // namespace fedmx

@@ -32,120 +32,66 @@
 // epilogue write-back.
 #include "fedmx_train_common.h"
 
-// Timing-only ablations of the main waves' step (WRONG numerics, never a
-// production build): 2 = no loss accumulation, 4 = no small-tile gradient /
-// Adam, 8 = every prefetch reads the epoch's first chunk (cache-resident:
-// what the prefetch's memory latency costs), 16 = helpers skip W4's Adam
-// (G4 folded in with one FMA per parameter), 32 = mains skip W1's Adam
-// (same), 64 = helpers do nothing between the barriers.  (1 = no per-step Adam constants on the mains, -6.3 %, led to the
-// helper-side computation below.)
-#ifndef FEDMX_HW_ABLATE
-#define FEDMX_HW_ABLATE 0
-#endif
-// 1: X's bias column DP-1 is read from memory (the packed training /
-// validation rows store the constant 1 there) instead of being set after each
-// load
-#ifndef FEDMX_HW_XBIAS
-#define FEDMX_HW_XBIAS 1
-#endif
-// 1: the Adam updates without FedProx in packed-fp32 form (adam4_packed)
-#ifndef FEDMX_HW_PACKED
-#define FEDMX_HW_PACKED 0
-#endif
-// 1: scaled-moment Adam (adam4s, fedmx_train_common.h) for W1, the small
-// tiles and W4: the moments live in registers as m/(1-b1), v/(1-b2) for the
-// whole launch (scaled after the prologue staging, unscaled before the
-// write-back), 7 instead of 10 VALU issues per parameter on a step that is
-// SIMD-issue bound (VERDICT r4 Next #1a).  The IEEE-Adam build
-// (FEDMX_EXACT_ADAM) keeps torch's unscaled rounding sequence.
-#ifndef FEDMX_HW_SCALED
-#define FEDMX_HW_SCALED (!FEDMX_EXACT_ADAM)
-#endif
-#if FEDMX_HW_SCALED && FEDMX_EXACT_ADAM
-#error "FEDMX_HW_SCALED rounds differently from torch; the IEEE-Adam build needs FEDMX_HW_SCALED=0"
-#endif
-// 1: barrier #1 is a main-waves-only LDS flag exchange and each helper hands
-// W4(s+1) / its Adam scalars to its main wave through an LDS flag the main
-// waits on right before layer 4, instead of through barrier #1.  The
-// helpers then no longer gate the mains' layer-1 exchange: their W4 gradient
-// + Adam window runs from barrier #2 of step s to layer 4 of step s+1.
-// 2: barrier #2 as well: the mains exchange their dH3 partials through LDS
-// flags and each helper starts on its main's dY^T / H3^T as soon as that
-// main has written them (no workgroup barrier left in the step loop).
-#ifndef FEDMX_HW_FLAGS
-#define FEDMX_HW_FLAGS 0
-#endif
-// 1: the constant-1 "bias units" of H1, Z and H3 (the slots that feed b2, b3
-// and b4 through the next layer's bias column) come out of the products
-// themselves instead of being set by a select after every product: inside
-// the launch W1's bias row, W2's bias row and W3's bias row hold a single 1
-// (in the input-bias column, the H1-bias column and the Z-bias column), so
-// relu(1 * 1) = 1, 1 * 1 = 1 and relu(1 * 1) = 1 exactly; W4's row of the
-// input-bias "feature" holds a 1 in the H3-bias column, so X's constant-1
-// column is reconstructed exactly and needs no mask in the loss and dY.
-// Their gradients are zero (the dH1 / dZ / dH3 masks already exclude the
-// bias slots; the bias feature's dY is exactly 0), so Adam
-// never moves them; the global parameters (aggregation, checkpoints) never
-// see them: set on staging in, cleared on staging out (bias_units_*).
-//
-// These three switches are bit masks over the kernel's instantiations -- bit
-// 0: batch <= 12 without FedProx (the benchmark's), bit 1: batch <= 12 with
-// FedProx, bit 2: MULTI (batch > 12, either) -- because the same removal of
-// VALU work measured faster in one and slower in another (r5 A/B, one box,
-// two passes, train launch us: plain / FedProx / batch 64):
+// Per-instantiation choices.  Each is a bit mask over the kernel's
+// instantiations -- bit 0: batch <= 12 without FedProx (the benchmark's),
+// bit 1: batch <= 12 with FedProx, bit 2: MULTI (batch > 12, either) --
+// because the same removal of VALU work measured faster in one and slower in
+// another (r5 A/B, one box, two passes, train launch us: plain / FedProx /
+// batch 64):
 //   scaled Adam only       885.5 / 973 / 698.5
 //   + bias units + masks   900.5 / 953 / 680
 //   + ping-pong            877.5 / 977 / 696.5
 //   + all three            889   / 986 / 661
 // so each instantiation gets its fastest combination.
-#ifndef FEDMX_HW_BIAS_UNITS
-#define FEDMX_HW_BIAS_UNITS 6
-#endif
-// 1: the backward masks test values, not slot tables: every padded hidden /
-// latent slot holds exactly 0 (zero weights, relu(0) = 0, zero gradients),
-// so "real and positive" is "positive" except at the one bias slot, which a
-// per-lane threshold (2 > the bias unit's 1) or a single-slot select
-// excludes: one compare + select per element instead of compare + scalar AND
-// + select, and no select at all on the latent axis but the bias slot's
-#ifndef FEDMX_HW_VALUE_MASKS
-#define FEDMX_HW_VALUE_MASKS 6
-#endif
-// 1: the step loop unrolled by two with the current / prefetched chunk
+//
+// BIAS_UNITS: the constant-1 "bias units" of H1, Z and H3 (the slots that feed
+// b2, b3 and b4 through the next layer's bias column) come out of the products
+// themselves instead of being set by a select after every product: inside the
+// launch W1's bias row, W2's bias row and W3's bias row hold a single 1 (in the
+// input-bias column, the H1-bias column and the Z-bias column), so
+// relu(1 * 1) = 1, 1 * 1 = 1 and relu(1 * 1) = 1 exactly; W4's row of the
+// input-bias "feature" holds a 1 in the H3-bias column, so X's constant-1
+// column is reconstructed exactly and needs no mask in the loss and dY.  Their
+// gradients are zero (the dH1 / dZ / dH3 masks already exclude the bias slots;
+// the bias feature's dY is exactly 0), so Adam never moves them; the global
+// parameters (aggregation, checkpoints) never see them: set on staging in,
+// cleared on staging out (bias_units_*).
+constexpr int BIAS_UNITS = 6;
+// VALUE_MASKS: the backward masks test values, not slot tables: every padded
+// hidden / latent slot holds exactly 0 (zero weights, relu(0) = 0, zero
+// gradients), so "real and positive" is "positive" except at the one bias
+// slot, which a per-lane threshold (2 > the bias unit's 1) or a single-slot
+// select excludes: one compare + select per element instead of compare +
+// scalar AND + select, and no select at all on the latent axis but the bias
+// slot's
+constexpr int VALUE_MASKS = 6;
+// PINGPONG: the step loop unrolled by two with the current / prefetched chunk
 // buffers swapping roles (instead of copying the prefetched chunk's 16
 // registers into the current one after every step)
-#ifndef FEDMX_HW_PINGPONG
-#define FEDMX_HW_PINGPONG 5
-#endif
-// the L2 / dZ products as two accumulator chains (chain2 below; the same
-// mask in fedmx_train.hip keeps the two kernels bit-identical).  r5h A/B:
-// plain -0.7 %, batch 64 -0.3 %, FedProx +1.2 % (profiles/r5_train_kernel_ab.md)
-#ifndef FEDMX_SPLIT_CHAINS
-#define FEDMX_SPLIT_CHAINS 5
-#endif
-// the same switch for the FedProx instantiation: 1 there (r4 A/B: FedProx
+constexpr int PINGPONG = 5;
+// SPLIT_CHAINS (fedmx_train.hip, the same mask keeps the two kernels
+// bit-identical): the L2 / dZ products as two accumulator chains (chain2)
+// W4FLAG_ROLES: the FedProx instantiation hands W4(s+1) and each step's Adam
+// scalars from helper w to main w through an LDS flag the main waits on right
+// before layer 4, and barrier #1 is a main-waves-only LDS flag exchange: the
+// helpers then no longer gate the mains' layer-1 exchange (r4 A/B: FedProx
 // launch -3.3 %, the plain launch +6 % -- without FedProx the helpers' path is
 // short enough that the flag polls only add latency to the mains')
-#ifndef FEDMX_HW_FLAGS_PROX
-#define FEDMX_HW_FLAGS_PROX 1
-#endif
-// (Round 4 also measured, and removed, four more variants of this step: a
-// software-pipelined W1 Adam / layer-1 (+4.2 %), the SPLIT step with layer 1's
-// second hidden tile and its backward on the helpers (+22.6 %), the eight dH3
-// partial reads issued together (+6.5 %, LDS issue stalls) and a co-simulation
-// probe; profiles/r4_train_hw_experiments.md, source in git history before
-// this note.)
-#ifndef FEDMX_HW_IGLP
-#define FEDMX_HW_IGLP 0   // the step loop's iglp_opt strategy (-1: none; r4 A/B: +12.6 %, 1: +1.6 %;
-                          // a second hint in the forward segment or the helpers' step: neutral)
-#endif
+constexpr int W4FLAG_ROLES = 2;
 // bound on one flag wait (polls); a wait that runs out marks the launch failed
 // (epochs_run = -1000) instead of hanging the GPU
 // (~1 ms of polls, vs ~3 us for a whole training step; after one wait has run
 // out the wave waits no more, so a broken hand-off ends the launch quickly)
-#ifndef FEDMX_HW_SPIN_LIMIT
-#define FEDMX_HW_SPIN_LIMIT (1 << 16)
-#endif
-constexpr int HW_SPIN_LIMIT = FEDMX_HW_SPIN_LIMIT;
+constexpr int HW_SPIN_LIMIT = 1 << 16;
+// (Rounds 3-5 also measured, and removed: a software-pipelined W1 Adam /
+// layer-1 (+4.2 %), layer 1's second hidden tile and its backward on the
+// helpers (+22.6 %), the eight dH3 partial reads issued together (+6.5 %),
+// iglp_opt(1) / no scheduling hint (+1.6 / +12.6 %), a step loop with no
+// workgroup barrier at all (LDS flags for barrier #2 too), packed-fp32 Adam
+// (+2 %), X's bias column set after each load instead of stored in the packed
+// rows, and the timing-only ablations of the step; source in git history,
+// numbers in profiles/r3_train_hw_experiments.md, r4_train_hw_experiments.md,
+// r5_train_kernel_ab.md.)
 
 // Asynchronous validation (TRAIN_FLAG_ASYNC_VALID, set by the launcher when
 // TrainArgs.vws is given and 2k workgroups fit the device at once): the
@@ -167,19 +113,12 @@ constexpr int HW_SPIN_LIMIT = FEDMX_HW_SPIN_LIMIT;
 // plain launch 874 -> 842 us, bench +3.5 %, paper configuration +4.6 %; the
 // FedProx and batch > 12 instantiations measured slower and keep the
 // synchronous epoch tail.
-#ifndef FEDMX_HW_ASYNC_VALID
-#define FEDMX_HW_ASYNC_VALID 1   // instantiation mask (bit 0 plain, bit 1 FedProx, bit 2 batch > 12)
-#endif
-#ifndef FEDMX_HW_AV_CHECK
-#define FEDMX_HW_AV_CHECK 6   // step of epoch e+1 before which the trainer needs epoch e's decision
-#endif
+constexpr int ASYNC_VALID = 1;   // instantiation mask (bit 0 plain, bit 1 FedProx, bit 2 batch > 12)
+constexpr int AV_CHECK = 6;      // step of epoch e+1 before which the trainer needs epoch e's decision
 // wall_clock64() ticks (100 MHz on gfx950) one cross-workgroup wait may take
 // before the launch reports itself failed (an epoch of a large client can
 // take many milliseconds; a validator that never runs must not hang the GPU)
-#ifndef FEDMX_HW_AV_TIMEOUT
-#define FEDMX_HW_AV_TIMEOUT 1000000000LL
-#endif
-constexpr int AV_CHECK = FEDMX_HW_AV_CHECK;
+constexpr long long AV_TIMEOUT = 1000000000LL;
 static_assert(AV_CHECK % 2 == 0, "the ping-pong step loop checks between step pairs");
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -269,7 +208,8 @@ __device__ __forceinline__ void av_st(unsigned long long* p, unsigned long long 
 // stamped `seq` and covers epoch need - 1, or AV_FAIL when the wait runs out.
 // (Inlined: a call anywhere in the step loop, even on its cold check branch,
 // makes the register allocator spill around it inside the loop.)
-__device__ __forceinline__ unsigned av_wait_decision(unsigned long long* dec, unsigned long long seq, int need) {
+__device__ __forceinline__ unsigned av_wait_decision(unsigned long long* dec, unsigned long long seq, int need,
+                                                     long long timeout) {
   const long long t0 = (long long)wall_clock64();
   for (;;) {
     const unsigned long long d = av_ld(dec);
@@ -277,7 +217,7 @@ __device__ __forceinline__ unsigned av_wait_decision(unsigned long long* dec, un
       const unsigned lo = (unsigned)d;
       if (lo == AV_FAIL || (int)((lo >> 1) & 0x7fffu) >= need) return lo;
     }
-    if ((long long)wall_clock64() - t0 > FEDMX_HW_AV_TIMEOUT) return AV_FAIL;
+    if ((long long)wall_clock64() - t0 > timeout) return AV_FAIL;
     __builtin_amdgcn_s_sleep(2);
   }
 }
@@ -316,7 +256,6 @@ struct Lane {
   float* own;
   int own_stride;
 };
-
 __device__ __forceinline__ void w1_to_lds(const MSlab& o, const Lane& L) {
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -358,7 +297,7 @@ __device__ __forceinline__ void lds_to_hslab(HSlab& o, const Lane& L) {
 }
 
 // asynchronous validation: a thread's Adam moments <-> its workspace record
-// (registers as they are: the scaled form of FEDMX_HW_SCALED included)
+// (registers as they are: the scaled form of ADAM_SCALED included)
 __device__ __forceinline__ f32x4 q4v(const float (&a)[4]) { return f32x4{a[0], a[1], a[2], a[3]}; }
 __device__ __forceinline__ void q4set(float (&a)[4], f32x4 v) {
 #pragma unroll
@@ -410,7 +349,7 @@ __device__ __forceinline__ void hslab_restore(const float* rec, HSlab& M, HSlab&
 }
 
 // compact-order product over the two halves of the hidden axis (7 k-steps).
-// SPLIT (FEDMX_SPLIT_CHAINS, per instantiation; fedmx_train.hip the same
+// SPLIT (SPLIT_CHAINS, per instantiation; fedmx_train.hip the same
 // order): each half in its own accumulator, interleaved, then added -- a
 // 4-long dependent MFMA chain instead of 7 (40-cycle result latency vs
 // 32-cycle issue) on the main waves' serial path (z after barrier #1, dZ
@@ -455,23 +394,23 @@ struct VTile {
 // instead of four.)
 template <bool PROX, bool MULTI>
 __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
-  // the flag hand-offs measured faster with FedProx only (profiles/r4_train_hw_experiments.md)
-  constexpr int HWF = MULTI ? 0 : (PROX ? FEDMX_HW_FLAGS_PROX : FEDMX_HW_FLAGS);
-  constexpr bool W4FLAG = HWF != 0;   // W4 / Adam scalars handed over by LDS flag (per-helper K slots)
+  // this instantiation's bit in the BIAS_UNITS, VALUE_MASKS, PINGPONG,
+  // SPLIT_CHAINS, W4FLAG_ROLES and ASYNC_VALID masks
+  constexpr int ROLE = MULTI ? 4 : (PROX ? 2 : 1);
+  // W4 / Adam scalars handed over by LDS flag (per-helper K slots), barrier #1
+  // a main-waves-only flag exchange
+  constexpr bool W4FLAG = (W4FLAG_ROLES & ROLE) != 0;
   constexpr bool CP = true;
   constexpr bool CPB = !MULTI;       // compact batch order (12 rows of 16 columns)
   constexpr int KB = CPB ? 3 : 4;    // k-steps of products over the batch
   constexpr int KZ = 2;   // k-steps of products over the latent axis
-  // this instantiation's bit in the FEDMX_HW_{BIAS_UNITS,VALUE_MASKS,PINGPONG} masks
-  constexpr int ROLE = MULTI ? 4 : (PROX ? 2 : 1);
-  constexpr bool BU = (FEDMX_HW_BIAS_UNITS & ROLE) != 0;
-  constexpr bool VMASK = (FEDMX_HW_VALUE_MASKS & ROLE) != 0;
-  constexpr bool PPONG = (FEDMX_HW_PINGPONG & ROLE) != 0;
-  constexpr bool SPLIT = (FEDMX_SPLIT_CHAINS & ROLE) != 0;
-  // asynchronous validation needs barrier #2 to be a workgroup barrier; it is
-  // a mask over the instantiations like the switches above (FedProx and
-  // batch > 12: their step loops spill registers with it compiled in)
-  constexpr bool AVOK = (FEDMX_HW_ASYNC_VALID & ROLE) != 0 && HWF < 2;
+  constexpr bool BU = (BIAS_UNITS & ROLE) != 0;
+  constexpr bool VMASK = (VALUE_MASKS & ROLE) != 0;
+  constexpr bool PPONG = (PINGPONG & ROLE) != 0;
+  constexpr bool SPLIT = (SPLIT_CHAINS & ROLE) != 0;
+  // asynchronous validation (a mask over the instantiations like the choices
+  // above: FedProx and batch > 12 measured slower with it compiled in)
+  constexpr bool AVOK = (ASYNC_VALID & ROLE) != 0;
   const bool av_launch = (A.flags & TRAIN_FLAG_ASYNC_VALID) != 0;   // grid: k trainers, then k validators
   const int nk = av_launch ? (int)gridDim.x / 2 : (int)gridDim.x;
   if (av_launch && !AVOK && (int)blockIdx.x >= nk) return;
@@ -501,11 +440,11 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   float* const sQ4 = sRedDH3 + L_RED + 4 * L_SCR;   // [w][v][t][lane][4]
   double* const sLoss = reinterpret_cast<double*>(sQ4 + L_Q4);  // [8 waves][4]
   // per-step Adam scalars (helper -> main), double-buffered by step parity:
-  // [neg_step_size, inv_bc2s, bc2s, -]; HWF: one pair per helper
+  // [kd, ed, -, -] (EXACT_ADAM: [neg_step_size, inv_bc2s, bc2s, -]); W4FLAG:
+  // one pair per helper
   float* const sK = reinterpret_cast<float*>(sLoss + 32);
-  // HWF: [0..3] layer-1 partials of step count v written by main w;
-  // [4..7] W4 / Adam scalars for step count v published by helper w;
-  // [8..11] (FLAGS 2) dH3 partial + dY^T / H3^T of step count v written by main w
+  // W4FLAG: [0..3] layer-1 partials of step count v written by main w;
+  // [4..7] W4 / Adam scalars for step count v published by helper w
   int* const sFlag = reinterpret_cast<int*>(sK + 32);
   // [12]: OR of every wave's spin_fail, read by thread 0 after the last barrier
   int* const sFail = sFlag + 12;
@@ -580,7 +519,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   int step = A.adam_step[cid];
   int parity = 0;
   const bool bias_lane = (w == 3 && g == 3);
-  const bool bias_col = (w == 3 && c == 15);
   const int xcol = 32 * w + 4 * g;
   const float lam = A.lambda;
   const float inv_d = 1.0f / (float)d_in;
@@ -601,7 +539,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     zreal_d[r] = j < latent;
     zbias_d[r] = j == z_bias_slot<CP>();
   }
-  // FEDMX_HW_VALUE_MASKS: the bias slots in the register tiles (compact
+  // VALUE_MASKS: the bias slots in the register tiles (compact
   // order): H3 / dH3 D-layout row 30 = tile 1, (g, r) = (3, 2); H1^T row 30 =
   // tile 1, column lane c = 14; Z D-layout row 13 = (g, r) = (3, 1)
   const float thr_h3b = (g == 3) ? 2.f : 0.f;
@@ -613,8 +551,9 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   for (int r = 0; r < 4; ++r) brow_b[r] = batch_row_of_col<CPB>(4 * g + r);
 
   // one batch chunk of X in both register layouts the step uses (f: layer
-  // 1's B operand over this wave's 32 columns; b: dW1's, batch on k);
-  // finalize_chunk then sets the bias column DP-1 to 1 (it feeds W1a's b1)
+  // 1's B operand over this wave's 32 columns; b: dW1's, batch on k).  The
+  // packed training / validation rows already hold the constant 1 in the
+  // bias column DP-1 (ClientStore._concat; it feeds W1a's b1).
   // Rows past the client's end (an epoch's last chunk) are read as they are:
   // the next client's rows or the buffer's zero tail (ClientStore), finite
   // values in batch columns every product masks.  So each load is a uniform
@@ -639,15 +578,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       x.b1[3] = 0.f;
     }
   };
-  // (FEDMX_HW_XBIAS: the packed rows already hold the 1 in column DP-1,
-  // ClientStore._concat -- nothing to overwrite after the load)
-  auto finalize_chunk = [&](XChunk& x) {
-    if (FEDMX_HW_XBIAS) return;
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-      if (bias_col) x.b1[r] = 1.f;
-    if (bias_lane) x.f1[3] = 1.f;
-  };
   // whole forward of one 16-row validation TILE by one wave (any of the 8).
   // The reference's validation loss is the mean over its batch-B DataLoader
   // batches of each batch's mean loss (`src/Trainer/client_trainer.py:387-404`):
@@ -671,7 +601,6 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) t.xf[b][v][r] = q[r];
       }
-    if (!FEDMX_HW_XBIAS && g == 3) t.xf[3][1][3] = 1.f;
   };
   auto valid_compute = [&](const VTile& t, int row0, int n_rows, double& lacc) {
     const int row = row0 + c;
@@ -805,13 +734,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   auto next_constants = [&]() {
     b1pow *= (double)A.beta1;
     b2pow *= (double)A.beta2;
-    if (FEDMX_HW_SCALED) {
-      adam_scaled_step(K, KI, b1pow, b2pow);
-    } else {
-      K.neg_step_size = (float)(-((double)A.lr / (1.0 - b1pow)));
-      K.bc2s = (float)sqrt(1.0 - b2pow);
-      K.inv_bc2s = 1.0f / K.bc2s;
-    }
+    adam_step_scalars(K, KI, A.lr, b1pow, b2pow);
   };
   // moment scales of adam4s (load: m / (1-b1), v / (1-b2); write-back: inverse)
   const float m_in = adam_moment_in_scale(A.beta1), v_in = adam_moment_in_scale(A.beta2);
@@ -877,7 +800,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     return worse >= A.patience && worse > 0;
   };
 
-  // ---- asynchronous validation (FEDMX_HW_ASYNC_VALID, see the top of the file)
+  // ---- asynchronous validation (ASYNC_VALID, see the top of the file)
   // (the workspace addresses are formed where they are used, from the kernel
   // arguments: nothing of this stays live through the step loop, whose
   // FedProx and batch > 12 instantiations sit at the register limit)
@@ -887,11 +810,15 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   auto av_dec = [&]() { return reinterpret_cast<unsigned long long*>(av_ws() + AV_L_M + 32); };
   auto av_rec = [&]() { return av_ws() + AV_L_M + AV_FLAGS + 40 * threadIdx.x; };
   auto av_seq = [&]() { return (unsigned long long)A.vseq << 32; };
+  // (TRAIN_FLAG_TEST_MUTE_VALIDATOR, tests only: 0.2 s instead of 10 s)
+  auto av_timeout = [&]() -> long long {
+    return (A.flags & TRAIN_FLAG_TEST_MUTE_VALIDATOR) ? AV_TIMEOUT / 50 : AV_TIMEOUT;
+  };
   bool av_break = false;   // the validator stopped the client: roll back to the last published epoch
   // (thread 0) the decision word's low half once it covers epoch need - 1, or AV_FAIL
   auto av_wait_dec = [&](int need) -> unsigned {
     if (spin_fail) return AV_FAIL;   // (one wait that ran out ends the launch's waiting)
-    const unsigned lo = av_wait_decision(av_dec(), av_seq(), need);
+    const unsigned lo = av_wait_decision(av_dec(), av_seq(), need, av_timeout());
     if (lo == AV_FAIL) spin_fail = true;
     return lo;
   };
@@ -950,8 +877,12 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   };
   // trainer, both roles: the masters of the last published epoch back into
   // LDS (the role restores its moments from av_rec after this; this thread's
-  // own stores of them are ordered before its loads)
+  // own stores of them are ordered before its loads).  The leading barrier
+  // orders the main waves' w1_to_lds of the discarded epoch (which a stop
+  // decided inside the step loop reaches without av_epoch_begin's barrier)
+  // before every wave's roll-back writes to the same LDS.
   auto av_rollback_lds = [&]() {
+    __syncthreads();
     const __amdgpu_buffer_rsrc_t rs = av_rsrc(av_ws());
     for (int i = threadIdx.x; i < AV_L_M / 4; i += 512) lds_write4(lds + 4 * i, av_load16(rs, i));
     __syncthreads();
@@ -961,6 +892,10 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   // (the synchronous epoch_tail's validation, loss order, patience rule and
   // best snapshot, on the trainer's published copy of each epoch)
   if (validator) {
+    // (TRAIN_FLAG_TEST_MUTE_VALIDATOR, tests only: client slot 0's validator
+    // never answers, so its trainer's decision wait runs out and the launch
+    // must report itself failed)
+    if ((A.flags & TRAIN_FLAG_TEST_MUTE_VALIDATOR) && kslot == 0) return;
     double min_v = __builtin_huge_val();
     int worse_v = 0, best_v = -1;
     // the validation rows do not change: each wave loads its (first two)
@@ -974,7 +909,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         const long long t0 = (long long)wall_clock64();
         int ok = 1;
         while (av_ld(av_ready()) != want) {
-          if ((long long)wall_clock64() - t0 > FEDMX_HW_AV_TIMEOUT) {
+          if ((long long)wall_clock64() - t0 > av_timeout()) {
             ok = 0;
             break;
           }
@@ -1060,7 +995,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     stage_vals(pv_v);
     lds_to_hslab(V4, L);
     __syncthreads();
-    if (FEDMX_HW_SCALED) {
+    if (ADAM_SCALED) {
 #pragma unroll
       for (int v = 0; v < 2; ++v)
 #pragma unroll
@@ -1085,20 +1020,20 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     };
     publish_q4();
     // The step's Adam scalars (f64 bias corrections: ~6 % of the main waves'
-    // step when they computed them, FEDMX_HW_ABLATE=1) are formed here one
+    // step when they computed them, r3 ablation) are formed here one
     // step ahead and handed over through LDS.
     int js = 0;   // step index within the launch
     auto publish_k = [&]() {
       next_constants();
-      const f32x4 kq = FEDMX_HW_SCALED ? f32x4{K.kd, K.ed, 0.f, 0.f} : f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f};
-      if (HWF) {
+      const f32x4 kq = ADAM_SCALED ? f32x4{K.kd, K.ed, 0.f, 0.f} : f32x4{K.neg_step_size, K.inv_bc2s, K.bc2s, 0.f};
+      if (W4FLAG) {
         if (lane == 0) lds_write4(sK + 8 * w + 4 * (js & 1), kq);
       } else if (lane == 0 && w8 == 4) {
         lds_write4(sK + 4 * (js & 1), kq);
       }
     };
     publish_k();   // step 0's
-    if (HWF) flag_set(4 + w, 1);   // W4 / scalars of launch step 0 published
+    if (W4FLAG) flag_set(4 + w, 1);   // W4 / scalars of launch step 0 published
     for (int ep = 0; ep < A.epochs; ++ep) {
       double acc_tr = 0.0;
       // W4 gradient + Adam between barrier #2 of step s and barrier #1 of s+1
@@ -1123,19 +1058,10 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
           }
         }
         HSTAMP(hs, 0);
-        if (!HWF) __syncthreads();   // barrier #1 (main: layer-1 partials)
+        if (!W4FLAG) __syncthreads();   // barrier #1 (main: layer-1 partials)
         HSTAMP(hs, 2);
-        if (HWF >= 2)
-          flag_wait(8 + w, 1, js + 1);   // main w's dY^T / H3^T of this step
-        else
-          __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
+        __syncthreads();   // barrier #2 (main: dY^T / H3^T of this step written)
         HSTAMP(hs, 7);
-        if (FEDMX_HW_ABLATE & 64) {
-          ++js;
-          publish_k();
-          if (HWF) flag_set(4 + w, js + 1);
-          continue;
-        }
         const f32x4 w4a0 = lds_read4(sT0 + tr);
         const f32x4 w4a1 = lds_read4(sT0 + tr + 16 * S_T);
         const f32x4 w4b0 = lds_read4(sT1 + tr);
@@ -1160,18 +1086,8 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 #pragma unroll
         for (int v = 0; v < 2; ++v)
 #pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            if (FEDMX_HW_ABLATE & 16) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) P4.q4[v][t][r] = __builtin_fmaf(G4[v][t][r], 0.f, P4.q4[v][t][r]);
-            } else if (FEDMX_HW_SCALED) {
-              adam4s<PROX>(P4.q4[v][t], M4.q4[v][t], V4.q4[v][t], AN4.q4[v][t], G4[v][t], K, prox_acc);
-            } else if (FEDMX_HW_PACKED && !PROX) {
-              adam4_packed(P4.q4[v][t], M4.q4[v][t], V4.q4[v][t], G4[v][t], K);
-            } else {
-              adam4<PROX>(P4.q4[v][t], M4.q4[v][t], V4.q4[v][t], AN4.q4[v][t], G4[v][t], K, prox_acc);
-            }
-          }
+          for (int t = 0; t < 2; ++t)
+            adam_update<PROX>(P4.q4[v][t], M4.q4[v][t], V4.q4[v][t], AN4.q4[v][t], G4[v][t], K, prox_acc);
         if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
         HSTAMP(hs, 10);
         // publish W4(s+1): master rows (layer 4, validation, snapshots) and the
@@ -1183,7 +1099,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         // (TRAIN_FLAG_TEST_DROP_W4, tests only: helper 0 never publishes launch
         // step 3's W4, so main wave 0's bounded wait for it runs out and the
         // launch must report itself failed)
-        if (HWF && !((A.flags & TRAIN_FLAG_TEST_DROP_W4) && w == 0 && js == 3))
+        if (W4FLAG && !((A.flags & TRAIN_FLAG_TEST_DROP_W4) && w == 0 && js == 3))
           flag_set(4 + w, js + 1);   // W4(js) ready for main w's layer 4
         HSTAMP(hs, 11);
       }
@@ -1215,7 +1131,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
     }
     // write back (barriers as the main branch; the mains stage to global)
-    if (FEDMX_HW_SCALED) {
+    if (ADAM_SCALED) {
 #pragma unroll
       for (int v = 0; v < 2; ++v)
 #pragma unroll
@@ -1253,7 +1169,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       for (int v = 0; v < 2; ++v) scale4(o.q1[t][v], sc);
     scale4(o.o, sc);
   };
-  if (FEDMX_HW_SCALED) {
+  if (ADAM_SCALED) {
     scale_mslab(M, m_in);
     scale_mslab(V, v_in);
   }
@@ -1296,14 +1212,13 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
     f32x4 l1a = zero4(), l1b = zero4();
     if (nb > 0) {
       load_chunk(Xtr, 0, min(B, n_tr), cur);
-      finalize_chunk(cur);
       l1_partial(cur, l1a, l1b);
     }
     int mb = 0, mch = 0;   // MULTI: batch / chunk of this step
     f32x4 G1[2][2], Go;
     // one training step on chunk `cur`, prefetching into `nxt`; the loop runs
     // it twice per iteration with the two chunk buffers' roles swapped (no
-    // 16-register copy of the prefetched chunk per step: FEDMX_HW_PINGPONG)
+    // 16-register copy of the prefetched chunk per step: PINGPONG)
     auto train_step = [&](const int bi, XChunk& cur, XChunk& nxt) {
       // MULTI: this step is chunk mch of batch mb (16 rows from row_b); the
       // batch's row count bt sets the scales, the chunk's bc the masks
@@ -1344,7 +1259,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         lds_write4(red + (w * 2 + 0) * 256 + lane * 4, l1a);
         lds_write4(red + (w * 2 + 1) * 256 + lane * 4, l1b);
         HSTAMP(ms, 1);
-        if (HWF) {
+        if (W4FLAG) {
           flag_set(w, js + 1);        // (release: the partial writes above complete first)
           flag_wait(0, 4, js + 1);    // every main wave's partial of this step
         } else {
@@ -1354,7 +1269,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         auto read_helper_state = [&]() {
           // this step's Adam scalars (helper-published)
           const f32x4 kk = lds_read4(W4FLAG ? sK + 8 * w + 4 * (js & 1) : sK + 4 * (js & 1));
-          if (FEDMX_HW_SCALED) {
+          if (ADAM_SCALED) {
             K.kd = kk[0];
             K.ed = kk[1];
           } else {
@@ -1456,10 +1371,10 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         norm_c = __builtin_amdgcn_sqrtf(nz);
         float contrib = sq * (inv_bt * inv_d);
         if (w == 0 && g == 0 && col_ok) contrib += lam * norm_c * inv_bt;
-        if (!(FEDMX_HW_ABLATE & 2)) acc_tr += (double)contrib;
+        acc_tr += (double)contrib;
         HSTAMP(ms, 3);
       }
-      if (has_next) load_chunk(Xtr, (FEDMX_HW_ABLATE & 8) ? 0 : row_n, bc_n, nxt);  // prefetch (ablation 8: chunk 0, cached)
+      if (has_next) load_chunk(Xtr, row_n, bc_n, nxt);  // prefetch
 
       float q2[2][4], q3[2][4];
 #pragma unroll
@@ -1503,12 +1418,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         sZT[tw + r * S_T] = zb[r];
       }
       HSTAMP(ms, 4);
-      if (HWF >= 2) {
-        flag_set(8 + w, js);        // js = this step's count + 1 (incremented before layer 4)
-        flag_wait(8, 4, js);        // every main wave's dH3 partial of this step
-      } else {
-        __syncthreads();  // barrier #2: dH3 partials of all waves visible
-      }
+      __syncthreads();  // barrier #2: dH3 partials of all waves visible
       HSTAMP(ms, 7);
       f32x4 dh3[2];
 #pragma unroll
@@ -1578,7 +1488,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
       wave_sync();
       // ---- owned small tile: w<2 -> dW3 tile = dH3^T Z ; w>=2 -> dW2 tile = dZ^T H1
-      if (!(FEDMX_HW_ABLATE & 4)) {
+      {
         const f32x4 a = lds_read4(sm_a);
         const f32x4 b = lds_read4(sm_b);   // (Z^T, or H1^T's tile of this wave)
 #pragma unroll
@@ -1586,16 +1496,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
       }
       HSTAMP(ms, 9);
       auto adam_w1 = [&](int t, int v) {
-        if (FEDMX_HW_ABLATE & 32) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) P.q1[t][v][r] = __builtin_fmaf(G1[t][v][r], 0.f, P.q1[t][v][r]);
-        } else if (FEDMX_HW_SCALED) {
-          adam4s<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
-        } else if (FEDMX_HW_PACKED && !PROX) {
-          adam4_packed(P.q1[t][v], M.q1[t][v], V.q1[t][v], G1[t][v], K);
-        } else {
-          adam4<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
-        }
+        adam_update<PROX>(P.q1[t][v], M.q1[t][v], V.q1[t][v], AN.q1[t][v], G1[t][v], K, prox_acc);
       };
       {
         // W1 first: the next chunk's layer-1 product waits on it
@@ -1608,25 +1509,15 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
         }
         HSTAMP(ms, 10);
         // (after an epoch's last batch this works on a stale tile; unused)
-        finalize_chunk(nxt);
         l1_partial(nxt, l1a, l1b);
       }
       if (last_ch) {
-        if (!(FEDMX_HW_ABLATE & 4)) {
-          if (FEDMX_HW_SCALED)
-            adam4s<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
-          else if (FEDMX_HW_PACKED && !PROX)
-            adam4_packed(P.o, M.o, V.o, Go, K);
-          else
-            adam4<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
-        }
+        adam_update<PROX>(P.o, M.o, V.o, AN.o, Go, K, prox_acc);
         if (PROX) acc_tr += (double)A.mu * (double)prox_acc;
-        if (!(FEDMX_HW_ABLATE & 4)) own_to_lds(P, L);   // read by every wave after barrier #1
+        own_to_lds(P, L);   // read by every wave after barrier #1
       }
       HSTAMP(ms, 11);
-#if FEDMX_HW_IGLP >= 0
-      __builtin_amdgcn_iglp_opt(FEDMX_HW_IGLP);
-#endif
+      __builtin_amdgcn_iglp_opt(0);
     };
     // (asynchronous validation: the decision on epoch ep-1 before step
     // AV_CHECK, an even step, so the chunk buffers keep their roles)
@@ -1696,7 +1587,7 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
   HSTAMP(true, 30);
   __syncthreads();
   masters_to_global_o<CP, BU>(Pg, sW1, sW4, sW2, sW3);
-  if (FEDMX_HW_SCALED) {
+  if (ADAM_SCALED) {
     scale_mslab(M, K.one_m_b1);
     scale_mslab(V, K.one_m_b2);
   }
@@ -1754,9 +1645,9 @@ int fedmx_train_hw(const void* args, int k, hipStream_t stream) {
   // can be resident at once -- a trainer waits for its validator's decisions
   int grid = k;
   A.flags &= ~fedmx::TRAIN_FLAG_ASYNC_VALID;
-  const int hwf = multi ? 0 : (A.mu != 0.f ? FEDMX_HW_FLAGS_PROX : FEDMX_HW_FLAGS);   // the kernel's HWF
-  const int role = multi ? 4 : (A.mu != 0.f ? 2 : 1);                                 // the kernel's ROLE
-  if ((FEDMX_HW_ASYNC_VALID & role) && A.vws != nullptr && A.vseq != 0 && A.epochs >= 1 && hwf < 2) {
+  const int role = multi ? 4 : (A.mu != 0.f ? 2 : 1);   // the kernel's ROLE
+  // (the decision word packs epoch + 1 into 15 bits: ADVICE r5)
+  if ((ASYNC_VALID & role) && A.vws != nullptr && A.vseq != 0 && A.epochs >= 1 && A.epochs < 32767) {
     static int cus = 0;
     if (cus == 0) {
       int dev = 0;

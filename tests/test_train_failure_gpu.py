@@ -103,3 +103,62 @@ def test_device_round_blocks_adoption_after_failed_launch(tmp_path, monkeypatch)
     monkeypatch.setattr(_hip, "TRAIN_TEST_FLAGS", 0)
     with pytest.raises(RuntimeError, match="training launch failed"):
         fed.run_round()
+
+
+def test_engine_raises_when_a_validator_never_answers(monkeypatch):
+    """VERDICT r5 Next #2b: asynchronous validation (plain instantiation) with
+    client slot 0's validator workgroup muted (runtime test bit
+    TRAIN_FLAG_TEST_MUTE_VALIDATOR; the decision wait is 0.2 s under it).  Its
+    trainer's bounded wait runs out: that client reports -1000, the launch's
+    error word is set and the host raises; the other client's launch result
+    stands."""
+    from fedmse_decentralized_amd.engine.base import TrainHParams
+    from fedmse_decentralized_amd.ops import _hip
+
+    eng = _engine(0.0)
+    err = torch.zeros(1, dtype=torch.int32, device=eng.device)
+    eng.train_err_ptr = err.data_ptr()
+    monkeypatch.setattr(_hip, "TRAIN_TEST_FLAGS", _hip.TRAIN_FLAG_TEST_MUTE_VALIDATOR)
+    hp = TrainHParams(epochs=3, batch_size=12, lr=1e-3, shrink_lambda=5.0, fedprox_mu=0.0, patience=10 ** 6)
+    h = eng.train_launch([0, 1], hp)
+    torch.cuda.synchronize()
+    assert _hip.lib().fedmx_train_hw_last_grid() == 4, "validator workgroups expected"
+    er = np.array(h.tensors[1])
+    assert er.tolist() == [-1000, 3], er
+    assert int(err.item()) == 1
+    with pytest.raises(RuntimeError, match="decision wait"):
+        eng.train_collect(h)
+    monkeypatch.setattr(_hip, "TRAIN_TEST_FLAGS", 0)
+    err.zero_()
+    res = eng.train_collect(eng.train_launch([0, 1], hp))
+    assert res.epochs_run.tolist() == [3, 3]
+    assert int(err.item()) == 0
+
+
+def test_device_round_blocks_adoption_after_muted_validator(tmp_path, monkeypatch):
+    """The device protocol after a validator decision wait ran out: nobody is
+    elected, nothing aggregated or adopted, and the host raises next round."""
+    from fedmse_decentralized_amd import federation
+    from fedmse_decentralized_amd.federation import Federation
+    from fedmse_decentralized_amd.ops import _hip
+
+    federation._PREP_CACHE.clear()
+    fed = Federation(_cfg(tmp_path, update_types=["fedavg"], epoch=3), "hybrid", "fedavg", 0).setup()
+    dr = fed._fast
+    assert dr is not None, "device round expected on the HIP engine in fixed mode"
+    st = fed.engine.store
+    torch.cuda.synchronize()
+    before = st.params.clone()
+    monkeypatch.setattr(_hip, "TRAIN_TEST_FLAGS", _hip.TRAIN_FLAG_TEST_MUTE_VALIDATOR)
+    r = fed.run_round()
+    torch.cuda.synchronize()
+    rec = dr.all_rounds[r.round]
+    assert int(rec["report"][0]) == _hip.ELECT_TRAIN_FAILED
+    assert int(dr.err.item()) == 1
+    sel = set(r.selected)
+    for c in range(fed.N):
+        if c not in sel:
+            assert torch.equal(st.params[c], before[c]), c
+    monkeypatch.setattr(_hip, "TRAIN_TEST_FLAGS", 0)
+    with pytest.raises(RuntimeError, match="training launch failed"):
+        fed.run_round()

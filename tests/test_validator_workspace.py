@@ -52,3 +52,18 @@ def test_launch_number_wraps_past_zero(monkeypatch):
     b.vseq = 0xFFFFFFFE
     assert b.validator_workspace(1, n_rows=4)[1] == 0xFFFFFFFF
     assert b.validator_workspace(1, n_rows=4)[1] == 1   # never 0
+
+
+def test_ranks_sharing_a_device_get_no_validators(monkeypatch):
+    """ranks that share one GPU compete for its CUs, so a trainer's
+    validator may never be dispatched beside it; such launches keep the
+    synchronous epoch tail."""
+    assert not _hip.ranks_share_device({}, device_count=1)
+    assert not _hip.ranks_share_device({"WORLD_SIZE": "1"}, device_count=1)
+    assert _hip.ranks_share_device({"WORLD_SIZE": "8", "LOCAL_WORLD_SIZE": "8"}, device_count=1)
+    assert not _hip.ranks_share_device({"WORLD_SIZE": "8", "LOCAL_WORLD_SIZE": "8"}, device_count=8)
+    assert _hip.ranks_share_device({"WORLD_SIZE": "2", "FEDMX_DEVICE_INDEX": "0"}, device_count=8)
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("FEDMX_DEVICE_INDEX", "0")
+    b = _bufs(monkeypatch, cus=256)
+    assert b.validator_workspace(2, n_rows=10) == (None, 0)
