@@ -1,0 +1,69 @@
+"""Build A/B variants of the HIP library from patched copies of the kernel
+sources (the production sources carry no experiment switches since round 6).
+
+    python scripts/ab_build.py NAME [NAME ...]     # -> ops/lib/libfedmx_hip_NAME.so
+    bash scripts/ab_train.sh                        # (GPU box) times them, AB_LIBS="main NAME ..."
+
+Each variant is a list of (file, exact old text, new text) substitutions
+applied to a temporary copy of ``ops/csrc/hip``; a substitution whose old
+text is missing fails the build (a stale variant never times the production
+kernel by accident).
+"""
+from __future__ import annotations
+
+import shutil
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+from fedmse_decentralized_amd.ops import build  # noqa: E402
+
+HW = "fedmx_train_hw.hip"
+
+
+def _mask(name, old, new):
+    return (HW, f"constexpr int {name} = {old};", f"constexpr int {name} = {new};")
+
+
+VARIANTS = {
+    # per-instantiation masks (bit 0 plain, 1 FedProx, 2 batch > 12): r6 re-check
+    # of the r5 choice on the round-6 code
+    "bu7vm7": [_mask("BIAS_UNITS", 6, 7), _mask("VALUE_MASKS", 6, 7)],
+    "pp7": [_mask("PINGPONG", 5, 7)],
+    "all7": [_mask("BIAS_UNITS", 6, 7), _mask("VALUE_MASKS", 6, 7), _mask("PINGPONG", 5, 7)],
+    "w4flag3": [_mask("W4FLAG_ROLES", 2, 3)],
+    "av3": [("fedmx_train_hw.hip", "constexpr int ASYNC_VALID = 1;", "constexpr int ASYNC_VALID = 3;")],
+    "stamps": [],   # (built with -DFEDMX_STAMPS=1 below)
+}
+FLAGS = {"stamps": ["-DFEDMX_STAMPS=1"]}
+
+
+def build_variant(name: str) -> Path:
+    subs = VARIANTS[name]
+    src = build.CSRC / "hip"
+    with tempfile.TemporaryDirectory() as td:
+        dst = Path(td) / "hip"
+        shutil.copytree(src, dst)
+        for fname, old, new in subs:
+            p = dst / fname
+            text = p.read_text()
+            if text.count(old) != 1:
+                raise SystemExit(f"variant {name}: {fname} has {text.count(old)} copies of {old!r}")
+            p.write_text(text.replace(old, new))
+        target = build.LIBDIR / f"libfedmx_hip_{name}.so"
+        base = build._hip_flags(FLAGS.get(name, []))
+        cmd = [build.hipcc_path(), *base[:3], "-fPIC", "-shared", *base[3:], f"-I{dst}",
+               *map(str, sorted(dst.glob("*.hip"))), "-o", str(target)]
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        if r.returncode != 0:
+            raise SystemExit(f"variant {name} failed:\n{r.stdout[-3000:]}")
+    return target
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:]:
+        print("built", build_variant(n))

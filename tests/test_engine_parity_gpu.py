@@ -171,6 +171,10 @@ def test_bench_config_20_rounds_matches_oracle(tmp_path):
     print(f"bench config, {rounds} rounds: discrete agreement hip/oracle {h_hip} rounds, oracle/perturbed oracle "
           f"{h_oracle}; max |AUC hip - oracle| while agreeing {worst:.2e}; max per-round mean-AUC gap hip "
           f"{mean_gap:.2e}, perturbed oracle {mean_gap_oracle:.2e}")
-    assert h_hip >= min(h_oracle, rounds), (h_hip, h_oracle)
+    # at least as long as the oracle agrees with its own perturbed copy, and
+    # never fewer than MIN_AGREE rounds (h_oracle can be 0; round 5
+    # measured h_oracle 4 on the CPU, the HIP engine 15)
+    MIN_AGREE = 5
+    assert h_hip >= max(min(h_oracle, rounds), MIN_AGREE), (h_hip, h_oracle)
     assert worst < 5e-3
     assert mean_gap <= max(5e-3, 2 * mean_gap_oracle)

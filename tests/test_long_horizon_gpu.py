@@ -43,6 +43,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LOSS_RTOL = 1e-4
 TOL = (("params", 1e-3, 1e-5), ("best", 1e-3, 1e-5), ("adam_m", 1e-3, 1e-6), ("adam_v", 1e-3, 1e-9))
 SENS_FACTOR = 3.0
+# absolute ceilings on the sensitivity-based limits: SENS_FACTOR x
+# the largest divergence the CPU oracle showed from its 1-ulp-perturbed copies
+# over every perturbation, both clients and all four (mu, batch) cases
+# (profiles/r6_long_horizon_sensitivity.json, scripts/long_horizon_sensitivity.py:
+# loss 2.06e-4 relative, parameters 1.65e-4, Adam m 2.72e-2, v 7.71e-2 -- the
+# chaotic client 1 at FedProx, batch 12), rounded up: a kernel regression of
+# chaotic size cannot pass by drawing a wider perturbation
+SENS_CEIL = {"loss_rel": 6.5e-4, "params": 5e-4, "best": 5e-4, "adam_m": 8.5e-2, "adam_v": 0.24}
 
 
 def _clients(seed=3):
@@ -122,14 +130,14 @@ def _violations(r1, ref, r2, hip, sens):
     for c in range(2):
         a, b = np.array(r1.tracking[c]), np.array(r2.tracking[c])
         rel = float(np.max(np.abs(b - a) / np.abs(a)))
-        lim = max(LOSS_RTOL, SENS_FACTOR * sens[c]["loss_rel"])
+        lim = max(LOSS_RTOL, min(SENS_FACTOR * sens[c]["loss_rel"], SENS_CEIL["loss_rel"]))
         if rel > lim:
             bad.append(f"client {c} losses rel {rel:.3g} > {lim:.3g}")
         for name, rtol, atol in TOL:
             x = getattr(hip.store, name)[c].cpu().double()
             y = getattr(ref.store, name)[c].double()
             d = (x - y).abs()
-            lim_abs = max(atol, SENS_FACTOR * sens[c][name])
+            lim_abs = max(atol, min(SENS_FACTOR * sens[c][name], SENS_CEIL[name]))
             over = d > (lim_abs + rtol * y.abs())
             if bool(over.any()):
                 bad.append(f"client {c} {name}: {int(over.sum())} entries beyond atol {lim_abs:.3g} + rtol {rtol} "
@@ -141,14 +149,16 @@ def _compare(r1, r2, ref, hip, clients, hp, report=None):
     """Kernel (r2, hip) against the oracle (r1, ref): exact epochs / best
     epoch / step counts; losses and tensors within the fixed floors, or, if a
     client exceeds them, within SENS_FACTOR x the largest divergence of the
-    oracle from a 1-ulp-perturbed copy of itself (_perturbations, tried in
-    turn until one accounts for the kernel's difference)."""
+    oracle from 1-ulp-perturbed copies of itself (every one of
+    _perturbations, always the whole set, and recorded), capped by
+    SENS_CEIL."""
     stats = {"epochs_run": [list(map(int, r1.epochs_run)), list(map(int, r2.epochs_run))],
              "best_epoch": [list(map(int, r1.best_epoch)), list(map(int, r2.best_epoch))],
              "kernel_vs_oracle": _diffs(r1, ref, r2, hip)}
     zero = {c: {"loss_rel": 0.0, **{name: 0.0 for name, _, _ in TOL}} for c in range(2)}
     sens, tried = zero, 0
     bad = _violations(r1, ref, r2, hip, sens)
+    per_pert = []
     if bad:
         for p_init in _perturbations(hp):
             p, _ = _engines(clients, None, p_init)
@@ -156,11 +166,10 @@ def _compare(r1, r2, ref, hip, clients, hp, report=None):
             r_p = p.train([0, 1], hp)
             tried += 1
             d = _diffs(r1, ref, r_p, p)
+            per_pert.append(d)
             sens = {c: {k: max(sens[c][k], d[c][k]) for k in sens[c]} for c in range(2)}
-            bad = _violations(r1, ref, r2, hip, sens)
-            if not bad:
-                break
-    stats.update(oracle_sensitivity=sens, perturbations_tried=tried)
+        bad = _violations(r1, ref, r2, hip, sens)
+    stats.update(oracle_sensitivity=sens, perturbations_tried=tried, per_perturbation=per_pert)
     print("long-horizon stats", json.dumps(stats), flush=True)   # on record even when an assertion fails
     if report is not None:
         report.update(stats)

@@ -143,7 +143,7 @@ def test_device_round_blocks_adoption_after_muted_validator(tmp_path, monkeypatc
     from fedmse_decentralized_amd.ops import _hip
 
     federation._PREP_CACHE.clear()
-    fed = Federation(_cfg(tmp_path, update_types=["fedavg"], epoch=3), "hybrid", "fedavg", 0).setup()
+    fed = Federation(_cfg(tmp_path, update_types=["avg"], epoch=3), "hybrid", "avg", 0).setup()
     dr = fed._fast
     assert dr is not None, "device round expected on the HIP engine in fixed mode"
     st = fed.engine.store
