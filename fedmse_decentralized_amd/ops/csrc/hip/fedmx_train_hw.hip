@@ -178,13 +178,42 @@ constexpr int AV_R = 512 * 40;
 constexpr int AV_SLOT = AV_L_M + AV_FLAGS + AV_R;
 static_assert(AV_L_M % 4 == 0 && AV_SLOT % 64 == 0, "workspace alignment");
 constexpr unsigned AV_FAIL = 0xffffffffu;   // decision word (low half) of a validator whose wait ran out
-// The hand-offs follow the write-through recipe (cdna_hip_programming.md §6
-// Guideline 16, R1 / R2): the snapshot is stored and loaded with sc1
-// (write-through, L1-bypassing) buffer accesses, every storing wave drains
-// its stores (s_waitcnt vmcnt(0)) before the workgroup barrier behind which
-// one lane stores the ready flag; flags and decisions are 8-byte relaxed
-// agent-scope atomics polled relaxed -- no L2 write-back or invalidate
-// (release / acquire fences: ~1.7-6.5 us each) anywhere.
+// Memory-model argument (VERDICT r5 Next #2c).  Trainer and validator run on
+// different CUs, usually on different XCDs, whose L2s are not coherent with
+// each other; each CU's vector L1 is never refreshed by another CU's stores.
+// The two hand-offs therefore follow the write-through recipe of
+// cdna_hip_programming.md §6 Guideline 16 and MI355X_MICROARCH.md
+// § visibility, which measures them valid without release / acquire fences
+// (each fence: ~1.7-6.5 us, an L2 write-back or L1 invalidate):
+//  * snapshot + FedProx term, trainer -> validator (R1, table row 1 "ONE lane
+//    of each storing workgroup, for ALL that workgroup's stores: an sc1 flag
+//    store"):  (1) EVERY store of the payload is sc1: 16-B
+//    raw_buffer_store_b128 with aux 16 (av_store16) for the masters, an 8-B
+//    relaxed agent-scope atomic store (global_store_dwordx2 sc1) for the
+//    FedProx term;  (2) every storing wave drains (s_waitcnt vmcnt(0),
+//    av_drain) before the workgroup barrier, and thread 0 then stores the
+//    ready flag -- after its own drain of the FedProx term -- as an 8-B
+//    relaxed agent-scope atomic (sc1);  (3) the validator's thread 0 polls
+//    the flag with relaxed agent-scope atomic loads (global_load_dwordx2 sc1),
+//    reads the FedProx term the same way after the match, and every other
+//    wave loads only behind the workgroup barrier thread 0 then joins;
+//    (4) EVERY load of the payload is an sc1 buffer load to registers
+//    (av_load16, raw_buffer_load_b128 aux 16: it bypasses the validator CU's
+//    L1, and sc1 makes the access coherent at agent scope, i.e. it is served
+//    from the memory side of the XCD L2s, where the trainer's write-through
+//    stores have landed before its flag).  The workspace is hipMalloc memory
+//    (the torch caching allocator) and both roles run one workgroup per CU
+//    (132 KB of LDS each): the row's memory / occupancy cells hold too.
+//  * decision, validator -> trainer (R2): the data is the flag -- one aligned
+//    8-B granule {launch number vseq, stop bit, epoch + 1, best epoch + 1}
+//    written by one relaxed agent-scope atomic store and polled by one
+//    relaxed agent-scope atomic load; the trainer uses nothing but the
+//    granule's own bits.  The best snapshot the validator writes (plain
+//    stores) is read only after the launch (kernel boundary).
+//  * the trainer's own moment records (av_rec) and its roll-back reads of the
+//    snapshot (sc1 loads of its own sc1 stores) stay on one CU.
+// Every wait is bounded (AV_TIMEOUT); a launch number per launch tags every
+// flag, so stale words of earlier launches never match (zeroed once).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t av_rsrc(float* p) {
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, AV_L_M * 4, 0x00020000);

@@ -55,3 +55,47 @@ def test_noniid_device_list_with_abnormal_less_clients(tmp_path):
         vals = r["client_metrics"]
         assert {names[i] for i, v in enumerate(vals) if v is None} == MISSING
         assert r["global_loss"] == min(v for v in vals if v is not None)
+
+
+KIT_CFG = "/root/reference/src/Configuration/kitsune-iot-10clients_noniid.json"
+
+
+def test_kitsune_noniid_device_list_missing_clients(tmp_path):
+    """VERDICT r5 Next #6b: the Kitsune non-IID list.  Client 5 ships without
+    ``abnormal/`` (loads; AUC null), client 7 without ``abnormal/`` and
+    ``normal/`` (no training data: the loader names the missing directory).
+    The list without client 7 -- the run of profiles/r6_noniid_kitsune.md
+    uses the 8 complete clients -- trains one round on the CPU engine."""
+    from fedmse_decentralized_amd import federation
+    from fedmse_decentralized_amd.config import ExperimentConfig
+    from fedmse_decentralized_amd.federation import Federation
+
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    from noniid_supervised_ceiling import derived_config
+
+    full = derived_config(KIT_CFG, [])
+    with pytest.raises(FileNotFoundError, match="Client-7/normal"):
+        federation._PREP_CACHE.clear()
+        Federation(ExperimentConfig(config_file=full, network_size=10, output_root=str(tmp_path / "a"),
+                                    backend="torch", device="cpu", log_level="WARNING"), "hybrid", "avg", 0).setup()
+    os.unlink(full)
+    path = derived_config(KIT_CFG, [7])
+    try:
+        federation._PREP_CACHE.clear()
+        cfg = ExperimentConfig(config_file=path, network_size=9, num_rounds=1, epoch=1, lr_rate=1e-3,
+                               shrink_lambda=1, output_root=str(tmp_path / "b"), backend="torch", device="cpu",
+                               compat="fixed", global_early_stop=False, save_checkpoints=False,
+                               log_level="WARNING", model_types=["hybrid"], update_types=["avg"])
+        fed = Federation(cfg, "hybrid", "avg", 0).setup()
+        by_name = {c.name: c for c in fed.clients}
+        assert len(by_name) == 9 and "Kitsune-Client-7" not in by_name
+        assert by_name["Kitsune-Client-5"].n_abnormal == 0
+        assert all(c.n_abnormal > 0 for n, c in by_name.items() if n != "Kitsune-Client-5")
+        r = fed.run_round()
+        m = np.asarray([np.nan if v is None else v for v in r.metrics], dtype=np.float64)
+        pos5 = [c.name for c in fed.clients].index("Kitsune-Client-5")
+        assert np.isnan(m[pos5]) and np.all(np.isfinite(np.delete(m, pos5)))
+        fed.finish()
+    finally:
+        os.unlink(path)
