@@ -49,6 +49,18 @@ class IpcUnavailable(RuntimeError):
     pass
 
 
+# spinning wait workgroups all co-located ranks may put on one GPU together
+# (half of a gfx950's ~2,048 resident 256-thread workgroups)
+WAIT_WORKGROUP_BUDGET = 1024
+
+
+def wait_chunk_cap(world: int, ranks_on_device: int, max_chunks: int) -> int:
+    """Chunks per source of one wait kernel such that the (chunks x world)
+    wait grids of every rank sharing this GPU stay within
+    WAIT_WORKGROUP_BUDGET (see _Channel)."""
+    return max(1, min(max_chunks, WAIT_WORKGROUP_BUDGET // (max(1, world) * max(1, ranks_on_device))))
+
+
 class _Channel:
     """One receive area per rank plus the sequence counter of its calls."""
 
@@ -64,6 +76,21 @@ class _Channel:
         self.world, self.rank = W, me
         self.slot_words = (int(slot_words) + 3) & ~3
         self.chunk_target = chunk_target
+        # Spinning wait workgroups must never fill the device: every rank's
+        # wait kernel is a (chunks x world) grid whose workgroups poll until
+        # the peers' push kernels have run, and ranks that SHARE one GPU
+        # (one-box rehearsals) each put such a grid on it.  A gfx950 device
+        # holds ~2,048 of these 256-thread workgroups at once (8 per CU); 8
+        # ranks x 8 sources x 64 chunks = 4,096 spinning workgroups left the
+        # peers' push kernels no CU to run on, every wait ran into its timeout
+        # and the self-test failed on every rank -- round 5's intermittent
+        # failure of the second bring-up of an 8-process rehearsal, whose
+        # larger federation (80 clients: 101K-word slots) needed 64 chunks
+        # where the first (27 chunks: 1,728 workgroups) still fitted.  The
+        # chunk count is capped so that all co-located ranks' wait grids
+        # together stay within half of that (1,024 workgroups); a rank alone
+        # on its GPU keeps up to IPC_MAX_CHUNKS.
+        self.max_chunks = wait_chunk_cap(W, comm.ranks_per_device(), _hip.IPC_MAX_CHUNKS)
         nbytes = 4 * (2 * W * self.slot_words + 2 * W * _hip.IPC_MAX_CHUNKS)
         hsz = self.L.fedmx_ipc_handle_size()
         handle = (ctypes.c_uint8 * hsz)()
@@ -132,7 +159,7 @@ class _Channel:
 
     def gather(self, out: torch.Tensor, t: torch.Tensor, stream: int) -> None:
         n = t.numel()
-        chunks = max(1, min(self.H.IPC_MAX_CHUNKS, -(-n // self.chunk_target)))
+        chunks = max(1, min(self.max_chunks, -(-n // self.chunk_target)))
         cw = ((-(-n // chunks)) + 3) & ~3
         a = self._args(t.data_ptr(), out.data_ptr(), n, chunks, cw)
         self.H._check(self.L.fedmx_ipc_push(ctypes.byref(a), stream), "fedmx_ipc_push")
@@ -184,6 +211,19 @@ class IpcComm(TorchDistComm):
     # the base (torch.distributed) object exchange, also used during bring-up
     def base_all_gather_object(self, obj):
         return TorchDistComm.all_gather_object(self, obj)
+
+    def ranks_per_device(self) -> int:
+        """How many ranks of the job run on this rank's physical GPU (the
+        collective self-test's device identities, or asked now); collective
+        when they are not known yet."""
+        ids = getattr(self, "peer_devices", None)
+        if ids is None:
+            from .launch import _device_identity
+
+            ids = self.base_all_gather_object(_device_identity(self.device))
+            self.peer_devices = ids
+        mine = ids[self.rank]
+        return max(1, sum(1 for i in ids if tuple(i) == tuple(mine)))
 
     def setup_exchange(self, gather_words: int, reduce_words: int) -> bool:
         """Create (or keep, when large enough) the two channels; collective.
