@@ -219,6 +219,19 @@ class DeviceRound:
             self._vdata = vdata
             self.vx = torch.tensor([d.data_ptr() for d in vdata], dtype=torch.int64, device=dev)
         self.fused_verify = bool(fed.local) and max(int(d.shape[0]) for d in vdata) <= _hip.VERIFY_MAX_ROWS
+        # split verification (fedmx_protocol.hip verify_split_kernel): each
+        # receiver's forward over ceil(tiles / 8) workgroups -- at most one
+        # 16-row tile per wave -- plus a drift workgroup; the thesis rule keeps
+        # the fused kernel (it forwards two models)
+        self.vsplit = None
+        if self.fused_verify and _hip.VERIFY_SPLIT and cfg.protocol_variant != "thesis":
+            tiles = max((int(d.shape[0]) + 15) // 16 for d in vdata)
+            self.vsplit_scratch = (torch.empty(self.n_local, _hip.VERIFY_MAX_ROWS, dtype=f32, device=dev),
+                                   torch.zeros(self.n_local, dtype=torch.int64, device=dev),
+                                   torch.zeros(self.n_local, dtype=i32, device=dev))
+            sse, drift, count = self.vsplit_scratch
+            self.vsplit = _hip.VerifySplitArgs(sse=sse.data_ptr(), drift=drift.data_ptr(), count=count.data_ptr(),
+                                               splits=max(1, min(64, -(-tiles // 8))), pad=0)
         # aggregation weights: 1 = FedMSE 1/MSE (device), 0 = plain mean,
         # 2 = sample-weighted FedAvg (host-computed: they depend on the selection only)
         # fusion_avg: weights formed on the device each round (rule 2 reads them
@@ -556,7 +569,10 @@ class DeviceRound:
                 v = _hip.VerifyArgs(D=d, vx=self.vx.data_ptr(), vn=self.vsse_n.data_ptr(),
                                     eval_params=eval_params.data_ptr(), best_stage=best_stage.data_ptr(),
                                     best=st.best.data_ptr(), latent=fed.dims.latent, hidden=fed.dims.hidden)
-                _hip.verify_decide(v, dev)
+                if self.vsplit is not None:
+                    _hip.verify_split(v, self.vsplit, dev)
+                else:
+                    _hip.verify_decide(v, dev)
             else:
                 _hip.decide_adopt(d, dev)
         slot_ptr, slot = self.rt.out.take(np.float64, 2 * N)

@@ -127,6 +127,18 @@ class VerifyArgs(ctypes.Structure):
                 ("best", _vp), ("latent", _i32), ("hidden", _i32)]
 
 
+class VerifySplitArgs(ctypes.Structure):
+    """fedmx_protocol.hip verify_split_kernel: per-receiver scratch (SSE rows,
+    drift granule, arrival counter) and the forward workgroups per receiver."""
+    _fields_ = [("sse", _vp), ("drift", _vp), ("count", _vp), ("splits", _i32), ("pad", _i32)]
+
+
+# split verification (round 6): the verification forward over several
+# workgroups per receiver, a drift workgroup beside them, the last arriver
+# decides; "0" keeps the one-workgroup-per-receiver fused kernel
+VERIFY_SPLIT = os.environ.get("FEDMX_VERIFY_SPLIT", "1") != "0"
+
+
 def lib():
     global _lib
     if _lib is not None:
@@ -156,6 +168,7 @@ def lib():
                 "fedmx_elect_wsum": [ctypes.POINTER(ElectArgs), ctypes.POINTER(WsumArgs), vp],
                 "fedmx_decide_adopt": [ctypes.POINTER(DecideArgs), vp],
                 "fedmx_verify_decide": [ctypes.POINTER(VerifyArgs), vp],
+                "fedmx_verify_split": [ctypes.POINTER(VerifyArgs), ctypes.POINTER(VerifySplitArgs), vp],
                 "fedmx_copy_f64": [vp, vp, i32, vp],
                 "fedmx_copy2_f64": [vp, vp, i32, vp, vp, i32, vp],
                 "fedmx_copy_rows": [vp, i32, vp, vp, i32, vp, i32, i32, vp],
@@ -185,6 +198,7 @@ def lib():
             assert tuple(sz) == (ctypes.sizeof(ElectArgs), ctypes.sizeof(WsumArgs), ctypes.sizeof(DecideArgs),
                                  ctypes.sizeof(VerifyArgs)), tuple(sz)
             assert L.fedmx_ipc_args_size() == ctypes.sizeof(IpcArgs)
+            assert L.fedmx_verify_split_args_size() == ctypes.sizeof(VerifySplitArgs)
             assert L.fedmx_ipc_max_world() == IPC_MAX_WORLD and L.fedmx_ipc_max_chunks() == IPC_MAX_CHUNKS
             _lib = L
     return _lib
@@ -644,6 +658,13 @@ def decide_adopt(args: DecideArgs, device):
 def verify_decide(args: VerifyArgs, device):
     """Verification forward + decide_adopt + evaluation snapshot, one launch."""
     _check(lib().fedmx_verify_decide(ctypes.byref(args), _stream(device)), "fedmx_verify_decide")
+
+
+def verify_split(args: VerifyArgs, sargs: VerifySplitArgs, device):
+    """verify_decide's decisions, adoption and snapshots with each receiver's
+    forward spread over ``sargs.splits`` workgroups and its drift over one
+    more (modes 0 / 1 / 3; the thesis rule keeps verify_decide)."""
+    _check(lib().fedmx_verify_split(ctypes.byref(args), ctypes.byref(sargs), _stream(device)), "fedmx_verify_split")
 
 
 def copy_f64(dst_ptr: int, src_ptr: int, n: int, device):

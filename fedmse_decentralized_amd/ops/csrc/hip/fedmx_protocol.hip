@@ -710,6 +710,271 @@ __global__ __launch_bounds__(512) void verify_decide_kernel(const VerifyArgs V) 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split verification (round 6, VERDICT r5 Next #7): the same decisions,
+// adoption and snapshots as verify_decide_kernel (modes 0 / 1 / 3: every
+// variant but the thesis rule), with each receiver's work spread over
+// `splits` forward workgroups and one drift workgroup instead of one
+// workgroup doing all of it in turn (r2 ablations of the fused kernel: the
+// forward 11.2 us, the drift 5.7 us, the adoption pass 3.2 us of 24.6).
+//
+//   workgroup (cl, p < splits): the aggregate's per-row SSE on rows
+//       [p T 16, (p+1) T 16) of receiver cl's verification data (T tiles per
+//       split; fwd_rows_block, so the rows' SSE are bit-identical to the
+//       fused kernel's), published to the scratch row block with sc1 stores;
+//   workgroup (cl, splits): the drift of cl's history against the aggregate
+//       (the fused kernel's code and order), published as one 8-byte granule;
+//   every workgroup then adds 1 to cl's arrival counter, and the LAST one
+//       (its add returned splits) reloads the SSE rows into LDS with sc1
+//       loads, reduces them in the fused kernel's order, decides, adopts and
+//       resets the counter to 0 for the next launch.
+// Hand-off (cdna_hip_programming.md §6 Guideline 16 R1; MI355X_MICROARCH.md
+// § visibility table row 1, "all those lanes add to ONE unsharded counter,
+// the workgroup whose add came last"): every storing wave drains its sc1
+// stores, then the workgroup barrier, then ONE lane's agent-scope atomic add;
+// the last arriver's other waves load after the barrier its lane then
+// joins, every load of the handed-off bytes an sc1 load; hipMalloc memory,
+// one workgroup of this kernel per CU at most (60 KB of LDS: 2 per CU fit,
+// the row allows one -- the scratch is written by one workgroup and read by
+// one, never by two on the same CU at once in one launch, so no L1 copy can
+// be stale).  No workgroup waits: the last arriver does the work, so the
+// grid needs no co-residency.
+struct VerifySplitArgs {
+  float* sse;                 // [n_local][VERIFY_MAX_ROWS] per-row SSE scratch
+  unsigned long long* drift;  // [n_local] granule {float drift, float history norm}
+  uint32_t* count;            // [n_local] arrivals; zero between launches (zeroed once; the last arriver resets)
+  int32_t splits;             // forward workgroups per receiver (>= 1)
+  int32_t pad;
+};
+static_assert(sizeof(VerifySplitArgs) == 32, "VerifySplitArgs layout is shared with Python");
+
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t vs_rsrc(float* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, bytes, 0x00020000);
+}
+
+template <bool CP, bool REL>
+__global__ __launch_bounds__(512) void verify_split_kernel(const VerifyArgs V, const VerifySplitArgs S) {
+  typedef __attribute__((address_space(1))) unsigned long long gu64;
+  typedef __attribute__((address_space(1))) uint32_t gu32;
+  const DecideArgs& A = V.D;
+  __shared__ __attribute__((aligned(16))) float sW1[HP * S_W1];
+  __shared__ __attribute__((aligned(16))) float sW2[ZP * S_W2];
+  __shared__ __attribute__((aligned(16))) float sW3[HP * S_W3];
+  __shared__ __attribute__((aligned(16))) float sW4[DP * S_W4];
+  __shared__ __attribute__((aligned(16))) float s_sse[VERIFY_MAX_ROWS];
+  __shared__ int s_ok, s_last;
+  __shared__ double s_d[4];
+  __shared__ float part[8][16];
+  __shared__ float part_h[8][16];
+  const int a = A.state[0];
+  const int per = S.splits + 1;
+  const int nver = A.n_local * per;
+  if (a >= 0 && blockIdx.x == 0 && threadIdx.x == 0) A.agg_counts[a] += 1;
+  if ((int)blockIdx.x >= nver) {
+    // the artefact snapshot best -> best_stage (as in verify_decide_kernel)
+    const int cl2 = blockIdx.x - nver;
+    if (cl2 >= A.n_local) return;
+    const size_t o2 = (size_t)cl2 * A.P;
+    const f32x4* b = reinterpret_cast<const f32x4*>(V.best + o2);
+    f32x4* bs = reinterpret_cast<f32x4*>(V.best_stage + o2);
+    for (int i = threadIdx.x; i < A.P / 4; i += blockDim.x) bs[i] = b[i];
+    return;
+  }
+  const int cl = blockIdx.x / per, role = blockIdx.x % per;
+  const int c = A.start + cl;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const size_t off = (size_t)cl * A.P;
+  const bool verifying = a >= 0 && A.mode != 1 && c != a;
+  const bool rel = REL && A.mode == 3;
+  const int had_hist = verifying ? A.has_hist[cl] : 0;   // (the last arriver updates it after every add)
+  const int n = V.vn[cl];
+  float* const sse_g = S.sse + (size_t)cl * VERIFY_MAX_ROWS;
+  if (verifying && role < S.splits) {
+    // ---- forward share: T tiles from tile role * T
+    const int ntiles = (n + 15) >> 4;
+    const int T = (ntiles + S.splits - 1) / S.splits;
+    const int row0 = min(n, role * T * 16);
+    const int nr = min(n - row0, T * 16);
+    if (nr > 0) {
+      FwdDesc d;
+      d.params = A.agg;
+      d.x = reinterpret_cast<const float*>(V.vx[cl]) + (size_t)row0 * DP;
+      d.sse = s_sse;
+      d.lat = nullptr;
+      d.nrows = nr;
+      d.lat_stride = V.latent;
+      d.d_in = A.d_in;
+      d.latent = V.latent;
+      d.hidden = V.hidden;
+      stage_params<CP>(A.agg, sW1, sW2, sW3, sW4);
+      __syncthreads();
+      fwd_rows_block<CP>(d, sW1, sW2, sW3, sW4, wv, 8, s_sse);
+      __syncthreads();
+      // publish the rows' SSE: 16-byte sc1 stores (row0 is a multiple of 16)
+      const __amdgpu_buffer_rsrc_t rs = vs_rsrc(sse_g + row0, 4 * ((nr + 3) & ~3));
+      for (int i = tid; i < (nr + 3) >> 2; i += 512)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, lds_read4(s_sse + 4 * i)), rs, 16 * i, 0,
+                                               16);
+    }
+  } else if (verifying && had_hist && (A.mode == 0 || rel)) {
+    // ---- drift (verify_decide_kernel's code and summation order)
+    const float* h = A.hist + off;
+    constexpr int NJ = (P_PAD + 1023) / 1024;
+    int sg[2][NJ];
+    float df[2][NJ], hv[2][NJ];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int p = tid + 512 * q + 1024 * j;
+        sg[q][j] = -1;
+        df[q][j] = 0.f;
+        hv[q][j] = 0.f;
+        if (p < P_PAD) {
+          sg[q][j] = A.seg[p];
+          hv[q][j] = h[p];
+          df[q][j] = hv[q][j] - A.agg[p];
+        }
+      }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float acc[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] = 0.f;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] += (sg[q][j] == t) ? df[q][j] * df[q][j] : 0.0f;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const float v = wave_sum(acc[t]);
+        if (lane == 0) part[t][wv + 8 * q] = v;
+      }
+      if (rel) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = 0.f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int t = 0; t < 8; ++t) acc[t] += (sg[q][j] == t) ? hv[q][j] * hv[q][j] : 0.0f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const float v = wave_sum(acc[t]);
+          if (lane == 0) part_h[t][wv + 8 * q] = v;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float tot = 0.f, toth = 0.f;
+      for (int t = 0; t < 8; ++t) {
+        float s2 = 0.f, h2 = 0.f;
+        for (int w = 0; w < 16; ++w) {
+          s2 += part[t][w];
+          if (rel) h2 += part_h[t][w];
+        }
+        tot += sqrtf(s2);
+        toth += sqrtf(h2);
+      }
+      const unsigned long long g = (unsigned long long)__builtin_bit_cast(uint32_t, tot) |
+                                   ((unsigned long long)__builtin_bit_cast(uint32_t, toth) << 32);
+      __hip_atomic_store((gu64*)(S.drift + cl), g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // ---- arrival: every storing wave drained, one lane adds; the last one decides
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t old = __hip_atomic_fetch_add((gu32*)(S.count + cl), 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == (uint32_t)(per - 1);
+    if (s_last) __hip_atomic_store((gu32*)(S.count + cl), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  bool ok = false, load = false;
+  if (a >= 0 && A.mode == 1) {
+    load = ok = true;   // centralised push: every hosted client loads and re-anchors
+  } else if (a >= 0 && c == a) {
+    load = true;   // the aggregator loads its aggregate (anchor / history unchanged)
+  } else if (a >= 0) {
+    // the rows' SSE back into LDS (sc1 loads), then the fused kernel's MSE order
+    {
+      const __amdgpu_buffer_rsrc_t rs = vs_rsrc(sse_g, 4 * ((n + 3) & ~3));
+      for (int i = tid; i < (n + 3) >> 2; i += 512)
+        lds_write4(s_sse + 4 * i, __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * i, 0, 16)));
+    }
+    __syncthreads();
+    double sv = 0.0;
+    if (tid < 256) {
+#pragma unroll 8
+      for (int r = tid; r < n; r += 256) sv += (double)s_sse[r];
+    }
+    for (int o = 32; o >= 1; o >>= 1) sv += __shfl_xor(sv, o, 64);
+    if (lane == 0 && wv < 4) s_d[wv] = sv;
+    __syncthreads();
+    const double tot = s_d[0] + s_d[1] + s_d[2] + s_d[3];
+    const double mse = n > 0 ? tot / ((double)n * A.d_in) : __builtin_nan("");
+    if (tid == 0) {
+      float drift = 0.f, hnorm = 0.f;
+      if (had_hist && (A.mode == 0 || rel)) {
+        const unsigned long long g = __hip_atomic_load((gu64*)(S.drift + cl), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        drift = __builtin_bit_cast(float, (uint32_t)g);
+        hnorm = __builtin_bit_cast(float, (uint32_t)(g >> 32));
+      }
+      const double perf = 1.0 / (1.0 + mse);
+      int okk;
+      if (!had_hist) {
+        okk = 1;  // the first received model is accepted unconditionally
+        A.has_hist[cl] = 1;
+      } else {
+        const double change = perf - A.hist_perf[cl];
+        const double lim = rel ? A.thr * (double)hnorm : A.thr;
+        okk = ((double)drift <= lim) && (change >= -A.pthr);
+      }
+      A.hist_perf[cl] = perf;
+      const int rj = okk ? 0 : A.rejected[cl] + 1;
+      A.rejected[cl] = rj;
+      A.rej_out[c] = (double)rj;
+      s_ok = okk;
+    }
+    __syncthreads();
+    ok = s_ok != 0;
+    load = ok;
+  }
+  // ---- adoption + history + snapshots in one pass over the row (as verify_decide_kernel)
+  const bool receiver = a >= 0 && c != a && (A.mode == 0 || A.mode == 3);
+  const int n4 = A.P / 4;
+  const f32x4* src = reinterpret_cast<const f32x4*>(A.agg);
+  f32x4* prm = reinterpret_cast<f32x4*>(A.params + off);
+  f32x4* evp = reinterpret_cast<f32x4*>(V.eval_params + off);
+  constexpr int UA = (P_PAD / 4 + 511) / 512;
+  f32x4 v[UA], pv[UA];
+#pragma unroll
+  for (int u = 0; u < UA; ++u) {
+    const int i = tid + 512 * u;
+    if (i < n4) {
+      v[u] = src[i];
+      pv[u] = load ? v[u] : prm[i];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UA; ++u) {
+    const int i = tid + 512 * u;
+    if (i < n4) {
+      if (load) {
+        prm[i] = v[u];
+        if (ok) reinterpret_cast<f32x4*>(A.anchor + off)[i] = v[u];
+      }
+      if (receiver) reinterpret_cast<f32x4*>(A.hist + off)[i] = v[u];
+      evp[i] = pv[u];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void copy_f64_kernel(double* __restrict__ dst, const double* __restrict__ src,
                                                        int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -782,6 +1047,32 @@ int fedmx_elect_wsum(const void* eargs, const void* wargs, hipStream_t stream) {
     hipLaunchKernelGGL(fedmx::elect_wsum_kernel<false>, dim3((W.P / 4 + 255) / 256), dim3(256), 0, stream, E, W);
   return (int)hipGetLastError();
 }
+
+// Split verification (modes 0 / 1 / 3); -5: the thesis rule (mode 2) needs
+// the fused kernel
+int fedmx_verify_split(const void* args, const void* sargs, hipStream_t stream) {
+  const fedmx::VerifyArgs& V = *reinterpret_cast<const fedmx::VerifyArgs*>(args);
+  const fedmx::VerifySplitArgs& S = *reinterpret_cast<const fedmx::VerifySplitArgs*>(sargs);
+  if (V.D.P % 4 != 0 || V.D.P != fedmx::P_PAD || S.splits < 1 || S.splits > 64) return -1;
+  if (V.D.mode == 2) return -5;
+  const int nl = V.D.n_local;
+  // n_local x (splits forward + 1 drift) workgroups, then n_local snapshot copies
+  const dim3 grid(nl > 0 ? nl * (S.splits + 1) + nl : 1);
+  const bool cp = V.D.d_in <= 115 && V.hidden <= 27 && V.latent <= 7;
+  if (V.D.mode == 3) {
+    if (cp)
+      hipLaunchKernelGGL((fedmx::verify_split_kernel<true, true>), grid, dim3(512), 0, stream, V, S);
+    else
+      hipLaunchKernelGGL((fedmx::verify_split_kernel<false, true>), grid, dim3(512), 0, stream, V, S);
+  } else if (cp) {
+    hipLaunchKernelGGL((fedmx::verify_split_kernel<true, false>), grid, dim3(512), 0, stream, V, S);
+  } else {
+    hipLaunchKernelGGL((fedmx::verify_split_kernel<false, false>), grid, dim3(512), 0, stream, V, S);
+  }
+  return (int)hipGetLastError();
+}
+
+int fedmx_verify_split_args_size(void) { return (int)sizeof(fedmx::VerifySplitArgs); }
 
 int fedmx_verify_decide(const void* args, hipStream_t stream) {
   const fedmx::VerifyArgs& V = *reinterpret_cast<const fedmx::VerifyArgs*>(args);
