@@ -19,9 +19,13 @@ export FEDMX_BENCH_EXTRA_TIMEOUT_S=${FEDMX_BENCH_EXTRA_TIMEOUT_S:-150}
 CARG=""
 [ "$COMM" = ipc ] && CARG="--comm ipc"
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
+# the per-rank traces stay outside gpurun_out (8 databases exceed what a call
+# copies back); the merged summary and the rank logs are kept
+TR=/tmp/fedmx_reh_$$
+mkdir -p $TR
 pids=""
 for r in $(seq 0 $((NR - 1))); do
-  RANK=$r LOCAL_RANK=$r timeout -k 10 400 rocprofv3 --kernel-trace -d $OUT/rank$r -o run \
+  RANK=$r LOCAL_RANK=$r timeout -k 10 400 rocprofv3 --kernel-trace -d $TR/rank$r -o run \
     -- python3 bench.py --gpus $NR --steps ${STEPS:-20} --warmup 5 $CARG ${EXTRA---no-extra} \
     --out $OUT/bench_rank$r.json > $OUT/rank$r.log 2>&1 &
   pids="$pids $!"
@@ -31,4 +35,6 @@ for p in $pids; do wait $p || rc=$?; done
 echo "ranks done rc=$rc"
 tail -n 2 $OUT/rank0.log | cut -c1-300
 [ $rc -ne 0 ] && exit $rc
-python3 scripts/rehearsal_trace_summary.py $OUT --out $OUT/summary.md > /dev/null && tail -n 30 $OUT/summary.md
+grep -h "peer-memory\|transport\|self-test\|fallback\|Traceback\|Error" $OUT/rank*.log | sort | uniq -c | head -n 20
+python3 scripts/rehearsal_trace_summary.py $TR --out $OUT/summary.md > /dev/null && tail -n 30 $OUT/summary.md
+rm -rf $TR

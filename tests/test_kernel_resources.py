@@ -54,7 +54,7 @@ def _loops(asm: str, fn: str):
         for t in b["br"]:
             if t in idx and idx[t] <= i:
                 seg = blocks[idx[t]:i + 1]
-                loops.append((sum(x["mfma"] for x in seg), sum(x["scratch"] for x in seg)))
+                loops.append((sum(x["mfma"] for x in seg), sum(x["scratch"] for x in seg), idx[t], i))
     return loops
 
 
@@ -66,7 +66,13 @@ def test_plain_training_kernel_register_budget():
     assert r["vgpr_spill"] <= 2, r
     assert r["scratch"] <= 16, r
     loops = _loops(res["__asm__"], PLAIN)
-    # the training-step loop: ping-pong of two steps, ~83 MFMAs each on the main waves
-    step_loops = [lp for lp in loops if lp[0] >= 150]
-    assert step_loops, loops
-    assert all(sc == 0 for _, sc in step_loops), f"scratch access inside the step loop: {step_loops}"
+    # the training-step loop: the innermost loop with >= 150 MFMAs (ping-pong
+    # of two steps, 83 each on the main waves; the epoch loop around it holds
+    # the epoch-end work and may reload a spilled offset there)
+    big = [lp for lp in loops if lp[0] >= 150]
+    inner = [lp for lp in big if not any(o is not lp and lp[2] <= o[2] and o[3] <= lp[3] and (o[2], o[3]) != (lp[2], lp[3])
+                                         for o in big)]
+    assert inner, loops
+    step = min(inner, key=lambda lp: lp[3] - lp[2])
+    assert 150 <= step[0] <= 200, step
+    assert step[1] == 0, f"scratch access inside the step loop: {step}"
