@@ -81,15 +81,12 @@ class _Channel:
         # the peers' push kernels have run, and ranks that SHARE one GPU
         # (one-box rehearsals) each put such a grid on it.  A gfx950 device
         # holds ~2,048 of these 256-thread workgroups at once (8 per CU); 8
-        # ranks x 8 sources x 64 chunks = 4,096 spinning workgroups left the
-        # peers' push kernels no CU to run on, every wait ran into its timeout
-        # and the self-test failed on every rank -- round 5's intermittent
-        # failure of the second bring-up of an 8-process rehearsal, whose
-        # larger federation (80 clients: 101K-word slots) needed 64 chunks
-        # where the first (27 chunks: 1,728 workgroups) still fitted.  The
-        # chunk count is capped so that all co-located ranks' wait grids
-        # together stay within half of that (1,024 workgroups); a rank alone
-        # on its GPU keeps up to IPC_MAX_CHUNKS.
+        # ranks x 8 sources x 64 chunks = 4,096 spinning workgroups could
+        # leave the peers' push kernels no CU to run on.  The chunk count is
+        # capped so that all co-located ranks' wait grids together stay
+        # within half of that (1,024 workgroups); a rank alone on its GPU keeps
+        # up to IPC_MAX_CHUNKS.  (Round 6 suspected this of round 5's failed
+        # second bring-up; the cap alone did not cure it -- IpcComm._teardown.)
         self.max_chunks = wait_chunk_cap(W, comm.ranks_per_device(), _hip.IPC_MAX_CHUNKS)
         nbytes = 4 * (2 * W * self.slot_words + 2 * W * _hip.IPC_MAX_CHUNKS)
         hsz = self.L.fedmx_ipc_handle_size()
@@ -171,6 +168,15 @@ class _Channel:
         self.H._check(self.L.fedmx_ipc_push(ctypes.byref(a), stream), "fedmx_ipc_push")
         self.H._check(self.L.fedmx_ipc_wait_reduce_f64(ctypes.byref(a), stream), "fedmx_ipc_wait_reduce_f64")
 
+    def retire(self) -> list:
+        """Detach this channel's memory without releasing it (see
+        IpcComm._teardown): returns [(kind, ptr)] for the final close."""
+        out = [("opened", q) for q in getattr(self, "opened", [])]
+        if getattr(self, "own", None):
+            out.append(("own", self.own))
+        self.opened, self.own = [], None
+        return out
+
     def close(self) -> None:
         from ..ops import _hiprt
 
@@ -197,6 +203,7 @@ class IpcComm(TorchDistComm):
 
         self.active = False
         self.ipc_calls = 0
+        self._retired: list = []   # [(kind, ptr)] of channels replaced by a larger bring-up
         self._gather: Optional[_Channel] = None
         self._reduce: Optional[_Channel] = None
         self._status = _hiprt.MappedBuffer(64)
@@ -310,12 +317,39 @@ class IpcComm(TorchDistComm):
             raise RuntimeError("peer-memory exchange: a wait timed out (a rank stalled or died); "
                                "rerun with FEDMX_COMM=rccl")
 
-    def _teardown(self):
+    def _teardown(self, release: bool = False):
+        """Drop the current channels.  A re-bring-up (a federation needing
+        larger slots) RETIRES them instead of freeing: round 6 reproduced round
+        5's failed second bring-up of an 8-process one-GPU rehearsal
+        (gpurun_out/s6: every peer's pushes never reached ONE rank's new
+        receive area, whose waits timed out) after freeing the first areas and
+        allocating new ones in the same processes; keeping every area and
+        peer mapping alive until the final close (a few MB) gives each
+        bring-up fresh allocations and fresh mappings.  ``release``: the final
+        close frees everything."""
         for ch in (self._gather, self._reduce):
-            if ch is not None:
+            if ch is None:
+                continue
+            if release:
                 ch.close()
+            else:
+                self._hip_sync()
+                self._retired += ch.retire()
         self._gather = self._reduce = None
         self.active = False
+        if release and self._retired:
+            L = self._hip.lib()
+            for kind, q in self._retired:
+                (L.fedmx_ipc_close if kind == "opened" else L.fedmx_ipc_free)(ctypes.c_void_p(q))
+            self._retired = []
+
+    def _hip_sync(self):
+        from ..ops import _hiprt
+
+        try:
+            _hiprt.device_sync()
+        except Exception:
+            pass
 
     # ---- the device protocol's two collectives ------------------------------------
     def all_gather_into(self, out, t):
@@ -339,4 +373,4 @@ class IpcComm(TorchDistComm):
         super().all_reduce_inplace(t)
 
     def close(self):
-        self._teardown()
+        self._teardown(release=True)
