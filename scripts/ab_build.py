@@ -37,6 +37,10 @@ VARIANTS = {
     "all7": [_mask("BIAS_UNITS", 6, 7), _mask("VALUE_MASKS", 6, 7), _mask("PINGPONG", 5, 7)],
     "w4flag3": [_mask("W4FLAG_ROLES", 2, 3)],
     "av3": [("fedmx_train_hw.hip", "constexpr int ASYNC_VALID = 1;", "constexpr int ASYNC_VALID = 3;")],
+    # FedProx with asynchronous validation and without the W4 LDS-flag hand-off
+    "av3nf": [("fedmx_train_hw.hip", "constexpr int ASYNC_VALID = 1;", "constexpr int ASYNC_VALID = 3;"),
+              _mask("W4FLAG_ROLES", 2, 0)],
+    "nf": [_mask("W4FLAG_ROLES", 2, 0)],
     "stamps": [],   # (built with -DFEDMX_STAMPS=1 below)
 }
 FLAGS = {"stamps": ["-DFEDMX_STAMPS=1"]}
