@@ -8,8 +8,7 @@ a host RNG whose consumption does not depend on results, so the whole round
 can be *enqueued* instead:
 
     train (fused kernel, all local selected clients)
-    forward + score_reduce -> vec[N,4] (vote score, dev MSE): one launch, each
-                            segment reduced by its last forward block
+    forward + score_reduce -> vec[N,4] (vote score, dev MSE)
                             [with collectives: records straight into the send
                             buffer's row 0, the pack of the selected models in
                             extra workgroups of the same launch]
@@ -233,9 +232,6 @@ class DeviceRound:
             sse, drift, count = self.vsplit_scratch
             self.vsplit = _hip.VerifySplitArgs(sse=sse.data_ptr(), drift=drift.data_ptr(), count=count.data_ptr(),
                                                splits=max(1, min(64, -(-tiles // 8))), pad=0)
-        # fused scoring (fedmx_forward.hip fwd_reduce_kernel): arrival counters
-        # of the vote / dev-set segments (<= 2 per hosted client), zero between launches
-        self.score_counts = torch.zeros(2 * self.n_local + 2, dtype=i32, device=dev) if _hip.FUSED_SCORE else None
         # aggregation weights: 1 = FedMSE 1/MSE (device), 0 = plain mean,
         # 2 = sample-weighted FedAvg (host-computed: they depend on the selection only)
         # fusion_avg: weights formed on the device each round (rule 2 reads them
@@ -443,16 +439,12 @@ class DeviceRound:
                     items += [(r, fed.dev_set) for r in local_rows]
                     outs += [p + 16 for p in recp]
                     batch += [0] * len(local_rows)
+                sse, _ = _hip.forward_rows(st.params, items, fed.dims, True, False)
                 # multi-rank: the exchange's pack (row 1 + j of the send buffer =
                 # the j-th local selection's parameters) rides the same launch
                 copies = [(st.params[self._loc(c)].data_ptr(), self.xsend[1 + j].data_ptr(), P_PAD)
                           for j, c in enumerate(local_sel)] if comm.collective and not _PACK_SEPARATE else ()
-                if self.score_counts is not None:
-                    # forward + reduction in one launch (the segment's last block reduces)
-                    _hip.forward_score_reduce_to(st.params, items, fed.dims, batch, outs, self.score_counts, copies)
-                else:
-                    sse, _ = _hip.forward_rows(st.params, items, fed.dims, True, False)
-                    _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs, copies)
+                _hip.score_reduce_to(sse, batch, fed.dims.d_in, outs, copies)
         with tel.phase("comm"):
             if not comm.collective:
                 base = st.params

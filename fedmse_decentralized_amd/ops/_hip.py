@@ -53,7 +53,7 @@ _lib_path: Optional[Path] = None
 FWD_DTYPE = np.dtype([
     ("params", "<u8"), ("x", "<u8"), ("sse", "<u8"), ("lat", "<u8"),
     ("nrows", "<i4"), ("lat_stride", "<i4"), ("d_in", "<i4"), ("latent", "<i4"),
-    ("hidden", "<i4"), ("seg", "<i4"), ("pad1", "<i8"),
+    ("hidden", "<i4"), ("pad0", "<i4"), ("pad1", "<i8"),
 ])
 CEN_DTYPE = np.dtype([
     ("train_lat", "<u8"), ("test_lat", "<u8"), ("out", "<u8"),
@@ -64,8 +64,6 @@ AUC_DTYPE = np.dtype([
     ("n", "<i4"), ("score_is_f64", "<i4"), ("score_scale", "<f4"), ("pad", "<i4"),
 ])
 SEG_DTYPE = np.dtype([("sse", "<u8"), ("n", "<i4"), ("batch", "<i4"), ("out", "<u8")])
-FUSED_SEG_DTYPE = np.dtype([("sse", "<u8"), ("n", "<i4"), ("batch", "<i4"), ("out", "<u8"), ("nblocks", "<i4"),
-                            ("pad", "<i4")])
 
 
 
@@ -135,21 +133,10 @@ class VerifySplitArgs(ctypes.Structure):
     _fields_ = [("sse", _vp), ("drift", _vp), ("count", _vp), ("splits", _i32), ("pad", _i32)]
 
 
-class FwdReduceArgs(ctypes.Structure):
-    """fedmx_forward.hip fwd_reduce_kernel: forward blocks, their segments
-    (SegDesc + live block count), arrival counters and riding row copies."""
-    _fields_ = [("descs", _vp), ("segs", _vp), ("count", _vp), ("copies", _vp), ("nfwd", _i32), ("nseg", _i32),
-                ("ncopy", _i32), ("d_in", _i32)]
-
-
 # split verification (round 6): the verification forward over several
 # workgroups per receiver, a drift workgroup beside them, the last arriver
 # decides; "0" keeps the one-workgroup-per-receiver fused kernel
 VERIFY_SPLIT = os.environ.get("FEDMX_VERIFY_SPLIT", "1") != "0"
-# fused scoring (round 6): the round's vote / dev-set forward and its score
-# reduction in one launch (last arriver per segment); "0" keeps forward_rows
-# then score_reduce
-FUSED_SCORE = os.environ.get("FEDMX_FUSED_SCORE", "1") != "0"
 
 
 def lib():
@@ -175,7 +162,6 @@ def lib():
                 "fedmx_auc": [vp, i32, vp],
                 "fedmx_score_reduce": [vp, i32, i32, vp],
                 "fedmx_score_reduce_copy": [vp, i32, i32, vp, i32, vp],
-                "fedmx_forward_reduce": [ctypes.POINTER(FwdReduceArgs), vp],
                 "fedmx_broadcast_rows": [vp, vp, vp, i32, vp, i32, vp],
                 "fedmx_train": [ctypes.POINTER(TrainArgs), i32, vp],
                 "fedmx_probe_mfma": [vp, vp],
@@ -213,7 +199,6 @@ def lib():
                                  ctypes.sizeof(VerifyArgs)), tuple(sz)
             assert L.fedmx_ipc_args_size() == ctypes.sizeof(IpcArgs)
             assert L.fedmx_verify_split_args_size() == ctypes.sizeof(VerifySplitArgs)
-            assert L.fedmx_forward_reduce_args_size() == ctypes.sizeof(FwdReduceArgs)
             assert L.fedmx_ipc_max_world() == IPC_MAX_WORLD and L.fedmx_ipc_max_chunks() == IPC_MAX_CHUNKS
             _lib = L
     return _lib
@@ -646,55 +631,6 @@ def score_reduce_to(sse_list: Sequence[torch.Tensor], batch: Sequence[int], d_in
         raise ValueError("score_reduce_to: copies must move whole float4 words")
     dptr, cptr = rt.desc.put(desc, cd)
     _check(lib().fedmx_score_reduce_copy(dptr, len(desc), d_in, cptr, len(cd), rt.stream), "fedmx_score_reduce_copy")
-
-
-def forward_score_reduce_to(params: torch.Tensor, items, dims, batch: Sequence[int], out_ptrs: Sequence[int],
-                            counts: torch.Tensor, copies: Sequence[Tuple[int, int, int]] = ()):
-    """forward_rows + score_reduce_to in ONE launch (fwd_reduce_kernel): each
-    item's rows are scored and, by the item's last forward block, reduced to
-    its (vote score, MSE) pair at ``out_ptrs[i]`` -- bit-identical to the two
-    launches.  ``counts``: int32 device arrivals, >= len(items) entries, zero
-    between launches (allocate zeroed once; the kernel resets them); launches
-    sharing a ``counts`` buffer must be stream-ordered.  Returns the SSE views."""
-    dev = params.device
-    _check_rows(items, dev)
-    if counts.dtype != torch.int32 or counts.device != dev or counts.numel() < len(items):
-        raise ValueError("forward_score_reduce_to: counts must be int32 on the params device, one per item")
-    sizes = np.array([int(x.shape[0]) for _, x in items], dtype=np.int64)
-    if len(items) == 0 or bool(np.any(sizes <= 0)):
-        # an empty segment has no block to reduce it: the two-launch path
-        sse, _ = forward_rows(params, items, dims, True, False)
-        score_reduce_to(sse, batch, dims.d_in, out_ptrs, copies)
-        return sse
-    rt = runtime(dev)
-    tot = int(sizes.sum())
-    sse_all = torch.empty(tot, dtype=torch.float32, device=dev)
-    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
-    P = params.shape[1]
-    pptr = params.data_ptr() + 4 * P * np.array([int(r) for r, _ in items], dtype=np.int64)
-    xptr = np.array([x.data_ptr() for _, x in items], dtype=np.int64)
-    sptr = sse_all.data_ptr() + 4 * offs
-    rpb = fwd_rows_per_block(tot, len(items))
-    item, _ = _fwd_layout(xptr, sizes, rpb)
-    desc = build_fwd_desc(pptr, xptr, sizes, sptr, np.zeros(len(items), np.int64), dims, rpb)
-    desc["seg"] = np.where(item >= 0, item, 0)
-    segs = np.zeros(len(items), dtype=FUSED_SEG_DTYPE)
-    segs["sse"] = sptr
-    segs["n"] = sizes
-    segs["batch"] = list(batch)
-    segs["out"] = np.asarray(out_ptrs, dtype=np.int64)
-    segs["nblocks"] = np.bincount(item[item >= 0], minlength=len(items))
-    cd = np.zeros(max(len(copies), 1), dtype=COPY_DTYPE)
-    if copies:
-        cd["src"] = [c[0] for c in copies]
-        cd["dst"] = [c[1] for c in copies]
-        cd["nfloats"] = [c[2] for c in copies]
-        if bool(np.any(cd["nfloats"] % 4)):
-            raise ValueError("forward_score_reduce_to: copies must move whole float4 words")
-    dptr, sgptr, cptr = rt.desc.put(desc, segs, cd)
-    args = FwdReduceArgs(dptr, sgptr, counts.data_ptr(), cptr, len(desc), len(items), len(copies), dims.d_in)
-    _check(lib().fedmx_forward_reduce(ctypes.byref(args), rt.stream), "fedmx_forward_reduce")
-    return [sse_all[o:o + n] for o, n in zip(offs, sizes)]
 
 
 def seg_desc_device(sse_list: Sequence[torch.Tensor], batch: Sequence[int], out_ptrs: Sequence[int], dev) -> torch.Tensor:

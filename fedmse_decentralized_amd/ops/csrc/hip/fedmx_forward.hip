@@ -12,7 +12,6 @@
 // 16-row tiles: 4 chained fp32 MFMA layers with the activations kept in
 // registers between layers (transposed orientation, see fedmx_common.h).
 #include "fedmx_forward_common.h"
-#include "fedmx_reduce_common.h"
 
 namespace fedmx {
 
@@ -33,83 +32,6 @@ __global__ __launch_bounds__(256) void fwd_rows_kernel(const FwdDesc* __restrict
     __syncthreads();
     fwd_rows_block<false>(d, sW1, sW2, sW3, sW4, threadIdx.x >> 6, 4, d.sse);
   }
-}
-
-// ---------------------------------------------------------------------------
-// Forward + score reduction in one launch (round 6, VERDICT r5 Next #7: the
-// round's vote / dev-set scoring was fwd_rows then score_reduce, two launches
-// back to back on the post-training chain).  Blocks < nfwd run fwd_rows'
-// blocks and publish their rows' SSE with sc1 stores; each then adds 1 to its
-// segment's arrival counter and the segment's LAST block (its add returned
-// nblocks - 1) reloads the segment with sc1 loads, staged through the
-// weights' LDS (score_reduce_staged), and reduces it in score_reduce's order (fedmx_reduce_common.h: bit-identical vote score and
-// MSE), resetting the counter to 0 for the next launch.  Blocks >= nfwd run
-// the row copies of score_reduce_copy.  Hand-off as verify_split_kernel's
-// (fedmx_protocol.hip; cdna_hip_programming.md §6 Guideline 16 R1): every
-// storing wave drains its sc1 stores, the workgroup barrier, ONE lane's
-// agent-scope add; no workgroup waits, so the grid needs no co-residency.
-struct FusedSeg {
-  SegDesc s;
-  int32_t nblocks;   // live forward blocks of the segment (> 0)
-  int32_t pad;
-};
-static_assert(sizeof(FusedSeg) == 32, "FusedSeg layout is shared with Python");
-
-struct FwdReduceArgs {
-  const FwdDesc* descs;     // [nfwd]; desc.seg = segment index (fillers: nrows <= 0)
-  const FusedSeg* segs;     // [nseg]; segs[i].s.sse = the segment's base in the descs' SSE buffer
-  uint32_t* count;          // [nseg] arrivals; zero between launches (zeroed once; the last arriver resets)
-  const CopyDesc* copies;   // [ncopy]
-  int32_t nfwd, nseg, ncopy, d_in;
-};
-static_assert(sizeof(FwdReduceArgs) == 48, "FwdReduceArgs layout is shared with Python");
-
-__global__ __launch_bounds__(256) void fwd_reduce_kernel(const FwdReduceArgs R) {
-  typedef __attribute__((address_space(1))) uint32_t gu32;
-  // the weights' LDS images; the last arriver reuses the space to stage its segment
-  constexpr int LDS_FLOATS = HP * S_W1 + ZP * S_W2 + HP * S_W3 + DP * S_W4;   // 10,048
-  constexpr int STAGE = 8192;
-  static_assert(STAGE <= LDS_FLOATS, "the reduction stages through the weights' LDS");
-  __shared__ __attribute__((aligned(16))) float s_lds[LDS_FLOATS];
-  float* const sW1 = s_lds;
-  float* const sW2 = sW1 + HP * S_W1;
-  float* const sW3 = sW2 + ZP * S_W2;
-  float* const sW4 = sW3 + HP * S_W3;
-  __shared__ double s_w[SCORE_WAVES];
-  __shared__ int s_last;
-  if ((int)blockIdx.x >= R.nfwd) {
-    copy_desc_block(R.copies[blockIdx.x - R.nfwd]);
-    return;
-  }
-  const FwdDesc d = R.descs[blockIdx.x];
-  if (d.nrows <= 0) return;   // alignment filler (not counted)
-  if (fwd_compact_ok(d)) {
-    stage_params<true>(d.params, sW1, sW2, sW3, sW4);
-    __syncthreads();
-    fwd_rows_block<true, true, true>(d, sW1, sW2, sW3, sW4, threadIdx.x >> 6, 4, d.sse);
-  } else {
-    stage_params<false>(d.params, sW1, sW2, sW3, sW4);
-    __syncthreads();
-    fwd_rows_block<false, true, true>(d, sW1, sW2, sW3, sW4, threadIdx.x >> 6, 4, d.sse);
-  }
-  // ---- arrival: every storing wave drained, one lane adds; the last one reduces
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const FusedSeg& fs = R.segs[d.seg];
-  if (threadIdx.x == 0) {
-    const uint32_t old = __hip_atomic_fetch_add((gu32*)(R.count + d.seg), 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == (uint32_t)(fs.nblocks - 1);
-    if (s_last) __hip_atomic_store((gu32*)(R.count + d.seg), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();   // (also: every wave is done with the weights' LDS)
-  if (!s_last) return;
-  const SegDesc sd = fs.s;
-  const __amdgpu_buffer_rsrc_t rs = sc1_rsrc(sd.sse, 4 * sd.n);
-  score_reduce_staged<256, STAGE>(
-      sd, R.d_in, s_w, s_lds,
-      [rs](int i) { return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, 4 * i, 0, SC1)); },
-      [rs](int i) { return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * i, 0, SC1)); });
 }
 
 // ---------------------------------------------------------------------------
@@ -195,15 +117,6 @@ int fedmx_forward_rows(const void* descs, int nblocks, hipStream_t stream) {
                      reinterpret_cast<const fedmx::FwdDesc*>(descs));
   return (int)hipGetLastError();
 }
-
-int fedmx_forward_reduce(const void* args, hipStream_t stream) {
-  const fedmx::FwdReduceArgs R = *reinterpret_cast<const fedmx::FwdReduceArgs*>(args);
-  if (R.nfwd + R.ncopy <= 0) return 0;
-  hipLaunchKernelGGL(fedmx::fwd_reduce_kernel, dim3(R.nfwd + R.ncopy), dim3(256), 0, stream, R);
-  return (int)hipGetLastError();
-}
-
-int fedmx_forward_reduce_args_size() { return (int)sizeof(fedmx::FwdReduceArgs); }
 
 int fedmx_weighted_sum(const float* stack, const float* w, int K, int P, float* out, hipStream_t stream) {
   if (P % 4 != 0) return -1;

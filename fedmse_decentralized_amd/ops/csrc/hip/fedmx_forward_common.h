@@ -17,7 +17,7 @@ struct FwdDesc {
   int32_t d_in;
   int32_t latent;
   int32_t hidden;
-  int32_t seg;          // fused forward + reduction: the block's segment (fwd_reduce_kernel); ignored elsewhere
+  int32_t pad0;
   int64_t pad1;
 };
 static_assert(sizeof(FwdDesc) == 64, "FwdDesc layout is shared with Python");
@@ -60,14 +60,6 @@ __device__ __forceinline__ int fwd_xcol(int d) {
     default: return d;
   }
 }
-// A buffer resource over `bytes` bytes at p, for the sc1 loads / stores of
-// the cross-workgroup hand-offs (cdna_hip_programming.md §6 Guideline 16 R1).
-typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sc1_rsrc(const float* p, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, bytes, 0x00020000);
-}
-constexpr int SC1 = 16;   // buffer instruction cache-policy bits: sc1
-
 constexpr int FWD_H_BIAS_POS = 30;   // fwd_hpos(HP - 1)
 constexpr int FWD_Z_BIAS_POS = 13;   // fwd_zpos(ZP - 1)
 
@@ -144,9 +136,8 @@ __device__ __forceinline__ void stage_params(const float* __restrict__ p, float*
 // at most one tile, which saves 32 VGPRs): 4 chained fp32
 // MFMA layers with the activations kept in registers between layers
 // (transposed orientation, see fedmx_common.h).  `sse` (global or LDS, row
-// indexed) receives per-row sums of squared error over d < d_in (PUBLISH:
-// global `sse`, written with sc1 stores for a last-arriver hand-off).
-template <bool CP, bool PREFETCH = true, bool PUBLISH = false>
+// indexed) receives per-row sums of squared error over d < d_in.
+template <bool CP, bool PREFETCH = true>
 __device__ __forceinline__ void fwd_rows_block(const FwdDesc& d, const float* sW1, const float* sW2,
                                                const float* sW3, const float* sW4, int wave, int nwaves,
                                                float* sse) {
@@ -271,13 +262,7 @@ __device__ __forceinline__ void fwd_rows_block(const FwdDesc& d, const float* sW
       }
     }
     part = sum_lane_groups(part);
-    if (PUBLISH) {
-      if (g == 0 && valid)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, part), sc1_rsrc(sse, 4 * d.nrows), 4 * row,
-                                              0, SC1);
-    } else if (g == 0 && valid) {
-      sse[row] = part;
-    }
+    if (g == 0 && valid) sse[row] = part;
   }
 }
 

@@ -748,6 +748,10 @@ struct VerifySplitArgs {
 };
 static_assert(sizeof(VerifySplitArgs) == 32, "VerifySplitArgs layout is shared with Python");
 
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t vs_rsrc(float* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, bytes, 0x00020000);
+}
 
 template <bool CP, bool REL>
 __global__ __launch_bounds__(512) void verify_split_kernel(const VerifyArgs V, const VerifySplitArgs S) {
@@ -809,10 +813,10 @@ __global__ __launch_bounds__(512) void verify_split_kernel(const VerifyArgs V, c
       fwd_rows_block<CP>(d, sW1, sW2, sW3, sW4, wv, 8, s_sse);
       __syncthreads();
       // publish the rows' SSE: 16-byte sc1 stores (row0 is a multiple of 16)
-      const __amdgpu_buffer_rsrc_t rs = sc1_rsrc(sse_g + row0, 4 * ((nr + 3) & ~3));
+      const __amdgpu_buffer_rsrc_t rs = vs_rsrc(sse_g + row0, 4 * ((nr + 3) & ~3));
       for (int i = tid; i < (nr + 3) >> 2; i += 512)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, lds_read4(s_sse + 4 * i)), rs, 16 * i, 0,
-                                               SC1);
+                                               16);
     }
   } else if (verifying && had_hist && (A.mode == 0 || rel)) {
     // ---- drift (verify_decide_kernel's code and summation order)
@@ -898,9 +902,9 @@ __global__ __launch_bounds__(512) void verify_split_kernel(const VerifyArgs V, c
   } else if (a >= 0) {
     // the rows' SSE back into LDS (sc1 loads), then the fused kernel's MSE order
     {
-      const __amdgpu_buffer_rsrc_t rs = sc1_rsrc(sse_g, 4 * ((n + 3) & ~3));
+      const __amdgpu_buffer_rsrc_t rs = vs_rsrc(sse_g, 4 * ((n + 3) & ~3));
       for (int i = tid; i < (n + 3) >> 2; i += 512)
-        lds_write4(s_sse + 4 * i, __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * i, 0, SC1)));
+        lds_write4(s_sse + 4 * i, __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * i, 0, 16)));
     }
     __syncthreads();
     double sv = 0.0;

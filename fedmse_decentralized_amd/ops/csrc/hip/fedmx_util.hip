@@ -11,24 +11,100 @@
 //      aggregate + refresh the FedProx anchor, client_trainer.py:191-195)
 //  * standardize_ddof1 (LDS-staged): vote-data normalisation
 //      (client_trainer.py:220-223)
-#include "fedmx_reduce_common.h"
+#include "fedmx_common.h"
 
 namespace fedmx {
 
-// One workgroup of 1024 threads per segment (fedmx_reduce_common.h).
+struct SegDesc {
+  const float* sse;  // [n]
+  int32_t n;
+  int32_t batch;     // rows per vote batch (128); <= 0: single batch
+  double* out;       // [2]: vote score, mean MSE
+};
+static_assert(sizeof(SegDesc) == 24, "SegDesc layout is shared with Python");
+
+constexpr int SCORE_THREADS = 1024;
+constexpr int SCORE_WAVES = SCORE_THREADS / 64;
+
+__device__ __forceinline__ double block_sum_d(double v, double* s_w) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lane == 0) s_w[wv] = v;
+  __syncthreads();
+  double r = 0.0;
+#pragma unroll
+  for (int w = 0; w < SCORE_WAVES; ++w) r += s_w[w];   // fixed order
+  __syncthreads();
+  return r;
+}
+
+// One workgroup of 1024 threads per segment.  A single-batch segment (the
+// dev-set MSE: 6.7K rows at 10 clients, 53K at 80) is summed with float4 loads,
+// four per thread in flight, so the latency-bound pass is a few round trips
+// instead of one per 256 rows; batched segments (the 128-row vote batches)
+// are reduced one batch after another.
 __device__ __forceinline__ void score_reduce_block(const SegDesc& d, int d_in) {
   __shared__ double s_w[SCORE_WAVES];
-  const float* p = d.sse;
-  score_reduce_seg<SCORE_THREADS>(
-      d, d_in, s_w, [p](int i) { return p[i]; },
-      [p](int i) { return *reinterpret_cast<const f32x4*>(p + i); });
+  const int tid = threadIdx.x;
+  const int bs = d.batch > 0 ? d.batch : (d.n > 0 ? d.n : 1);
+  const int nb = (d.n + bs - 1) / bs;
+  double vote = 0.0, tot = 0.0;
+  if (nb == 1) {
+    const float* p = d.sse;
+    const int n = d.n;
+    const int head = min(n, (int)((4 - ((reinterpret_cast<uintptr_t>(p) >> 2) & 3)) & 3));
+    const int n4 = (n - head) >> 2;
+    const f32x4* q = reinterpret_cast<const f32x4*>(p + head);
+    double s = 0.0;
+    if (tid < head) s += (double)p[tid];
+    int i = tid;
+    for (; i + 3 * SCORE_THREADS < n4; i += 4 * SCORE_THREADS) {
+      const f32x4 a = q[i], b = q[i + SCORE_THREADS], c = q[i + 2 * SCORE_THREADS], e = q[i + 3 * SCORE_THREADS];
+      s += (double)a[0]; s += (double)a[1]; s += (double)a[2]; s += (double)a[3];
+      s += (double)b[0]; s += (double)b[1]; s += (double)b[2]; s += (double)b[3];
+      s += (double)c[0]; s += (double)c[1]; s += (double)c[2]; s += (double)c[3];
+      s += (double)e[0]; s += (double)e[1]; s += (double)e[2]; s += (double)e[3];
+    }
+    for (; i < n4; i += SCORE_THREADS) {
+      const f32x4 a = q[i];
+      s += (double)a[0]; s += (double)a[1]; s += (double)a[2]; s += (double)a[3];
+    }
+    const int t0 = head + 4 * n4;
+    if (t0 + tid < n) s += (double)p[t0 + tid];
+    tot = block_sum_d(s, s_w);
+    vote = n > 0 ? tot / ((double)n * d_in) : 0.0;
+  } else {
+    for (int b = 0; b < nb; ++b) {
+      const int r0 = b * bs;
+      const int r1 = min(d.n, r0 + bs);
+      double s = 0.0;
+      for (int r = r0 + tid; r < r1; r += SCORE_THREADS) s += (double)d.sse[r];
+      s = block_sum_d(s, s_w);
+      tot += s;
+      vote += s / ((double)(r1 - r0) * d_in);
+    }
+  }
+  if (tid == 0) {
+    d.out[0] = nb > 0 ? vote / nb : __builtin_inf();
+    d.out[1] = d.n > 0 ? tot / ((double)d.n * d_in) : __builtin_nan("");
+  }
 }
 
 __global__ __launch_bounds__(SCORE_THREADS) void score_reduce_kernel(const SegDesc* __restrict__ descs, int d_in) {
   score_reduce_block(descs[blockIdx.x], d_in);
 }
 
-// row copies riding the same launch (CopyDesc, fedmx_reduce_common.h)
+// row copies riding the same launch (the multi-rank exchange's pack of the
+// locally selected models into the send buffer: it needs the trained
+// parameters only, so it runs beside the score reduction instead of as a
+// launch of its own on the round's critical path)
+struct CopyDesc {
+  const float* src;
+  float* dst;
+  int32_t nfloats;   // multiple of 4
+  int32_t pad;
+};
+static_assert(sizeof(CopyDesc) == 24, "CopyDesc layout is shared with Python");
 
 __global__ __launch_bounds__(SCORE_THREADS) void score_reduce_copy_kernel(const SegDesc* __restrict__ descs, int n,
                                                                           int d_in,
@@ -37,7 +113,10 @@ __global__ __launch_bounds__(SCORE_THREADS) void score_reduce_copy_kernel(const 
     score_reduce_block(descs[blockIdx.x], d_in);
     return;
   }
-  copy_desc_block(copies[blockIdx.x - n]);
+  const CopyDesc c = copies[blockIdx.x - n];
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(c.src);
+  f32x4* d4 = reinterpret_cast<f32x4*>(c.dst);
+  for (int i = threadIdx.x; i < c.nfloats / 4; i += SCORE_THREADS) d4[i] = s4[i];
 }
 
 __global__ __launch_bounds__(256) void broadcast_rows_kernel(float* __restrict__ dst0, float* __restrict__ dst1,

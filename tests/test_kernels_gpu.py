@@ -321,49 +321,3 @@ def test_forward_rows_independent_of_block_length():
         del os.environ["FEDMX_FWD_ROWS_PER_BLOCK"]
     for a, b in zip(sse_a, sse_b):
         assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("with_copies", [False, True])
-def test_fused_forward_score_reduce_matches_two_launches(with_copies):
-    """fwd_reduce_kernel (the round's vote / dev-set scoring in one launch,
-    each segment reduced by its last forward block) against forward_rows +
-    score_reduce: bit-identical per-row SSE, vote scores and MSEs over
-    segments of 1 .. 20,001 rows (batched by 128 / 64 / 7 / 3,000 / 9,000 and
-    single-batch: one and several LDS staging chunks, and the direct path of
-    batches larger than a chunk; segment starts off 16-byte alignment; items
-    sharing their rows, so the XCD-grouped layout inserts filler blocks), three launches on one counter
-    buffer (the last arriver's reset) and riding row copies."""
-    params, _ = init_client_params(5, 9)
-    params = params + 0.05 * torch.randn(params.shape, generator=torch.Generator().manual_seed(2))
-    pad = canonical_to_padded(params).to(DEV)
-    sizes = [1, 3, 17, 130, 777, 6700, 6700, 300, 20001, 20001, 20001, 9000]
-    batch = [128, 0, 64, 128, 0, 0, 128, 7, 0, 128, 9000, 3000]
-    xs = {n: _data(n, seed=n).to(DEV) for n in set(sizes)}
-    items = [(i % 5, xs[n]) for i, n in enumerate(sizes)]
-    n = len(items)
-    d_in = DEFAULT_DIMS.d_in
-    ref = torch.zeros(n, 2, dtype=torch.float64, device=DEV)
-    sse_ref, _ = _hip.forward_rows(pad, items, DEFAULT_DIMS, True, False)
-    _hip.score_reduce_to(sse_ref, batch, d_in, [ref[i].data_ptr() for i in range(n)])
-    counts = torch.zeros(n + 3, dtype=torch.int32, device=DEV)
-    for _ in range(3):
-        out = torch.full((n, 2), float("nan"), dtype=torch.float64, device=DEV)
-        dst = torch.zeros(3, P_PAD, dtype=torch.float32, device=DEV)
-        copies = [(pad[r].data_ptr(), dst[j].data_ptr(), P_PAD) for j, r in enumerate((4, 0, 2))] \
-            if with_copies else ()
-        sse = _hip.forward_score_reduce_to(pad, items, DEFAULT_DIMS, batch, [out[i].data_ptr() for i in range(n)],
-                                           counts, copies)
-        torch.cuda.synchronize()
-        assert torch.equal(out, ref), (out - ref).abs().max()
-        for a, b in zip(sse, sse_ref):
-            assert torch.equal(a, b)
-        assert int(counts.count_nonzero()) == 0
-        if with_copies:
-            assert torch.equal(dst, pad[[4, 0, 2]])
-    # and the reduction itself against float64 torch
-    for i, (s, b) in enumerate(zip(sse_ref, batch)):
-        sd = s.double().cpu()
-        bs = b if b > 0 else len(sd)
-        vote = torch.stack([c.sum() / (len(c) * d_in) for c in sd.split(bs)]).mean()
-        torch.testing.assert_close(ref[i].cpu(), torch.stack([vote, sd.sum() / (len(sd) * d_in)]),
-                                   rtol=1e-12, atol=0)
