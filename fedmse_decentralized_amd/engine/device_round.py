@@ -54,6 +54,10 @@ import torch
 from ..models.layout import P_PAD
 from ..ops import _hip
 
+# fence-less device events for the kernel-to-kernel stream dependencies
+# ("0": torch events, which record with a system-scope fence)
+_DEVICE_EVENTS = os.environ.get("FEDMX_DEVICE_EVENTS", "1") != "0"
+
 log = logging.getLogger("fedmx")
 
 
@@ -232,6 +236,11 @@ class DeviceRound:
             sse, drift, count = self.vsplit_scratch
             self.vsplit = _hip.VerifySplitArgs(sse=sse.data_ptr(), drift=drift.data_ptr(), count=count.data_ptr(),
                                                splits=max(1, min(64, -(-tiles // 8))), pad=0)
+        # the two per-round stream dependencies whose consumers are kernels only
+        # (side -> main: the standardised vote data; main -> side: the round's
+        # decisions and snapshots for the evaluation): fence-less device events
+        # (_hiprt.DeviceEvent), torch events with FEDMX_DEVICE_EVENTS=0
+        self.dev_ev = (_hip._hiprt.DeviceEvent(), _hip._hiprt.DeviceEvent()) if _DEVICE_EVENTS else None
         # aggregation weights: 1 = FedMSE 1/MSE (device), 0 = plain mean,
         # 2 = sample-weighted FedAvg (host-computed: they depend on the selection only)
         # fusion_avg: weights formed on the device each round (rule 2 reads them
@@ -403,8 +412,12 @@ class DeviceRound:
             vs = self.vs_bufs[pb][:vdata.shape[0]]
             with _hip.on_stream(self.side):
                 _hip.standardize_ddof1(vdata.contiguous(), fed.dims.d_in, out=vs)
-                ev_std = torch.cuda.Event()
-                ev_std.record(self.side)
+                if self.dev_ev is not None:
+                    ev_std = self.dev_ev[0]
+                    ev_std.record(self.side.cuda_stream)
+                else:
+                    ev_std = torch.cuda.Event()
+                    ev_std.record(self.side)
         with tel.phase("train"):
             tev = None
             if self.train_timing and local_sel:
@@ -422,7 +435,10 @@ class DeviceRound:
         with tel.phase("vote"):
             if local_sel:
                 if ev_std is not None:
-                    torch.cuda.current_stream(dev).wait_event(ev_std)
+                    if self.dev_ev is not None:
+                        ev_std.wait(torch.cuda.current_stream(dev).cuda_stream)
+                    else:
+                        torch.cuda.current_stream(dev).wait_event(ev_std)
                 need_dev = self.rule == 1
                 items = [(r, vs) for r in local_rows]
                 # each client's record [vote score, -, dev MSE, dev MSE] (4 doubles):
@@ -583,10 +599,17 @@ class DeviceRound:
             nd = st.params.numel() // 2
             _hip.copy2_f64(eval_params.data_ptr(), st.params.data_ptr(), nd,
                            best_stage.data_ptr(), st.best.data_ptr(), nd, dev)
-        ev_dec = torch.cuda.Event()
-        ev_dec.record()
+        if self.dev_ev is not None:
+            ev_dec = self.dev_ev[1]
+            ev_dec.record(torch.cuda.current_stream(dev).cuda_stream)
+        else:
+            ev_dec = torch.cuda.Event()
+            ev_dec.record()
         with tel.phase("eval"), _hip.on_stream(self.side):
-            self.side.wait_event(ev_dec)
+            if self.dev_ev is not None:
+                ev_dec.wait(self.side.cuda_stream)
+            else:
+                self.side.wait_event(ev_dec)
             if local_sel and cfg.save_checkpoints:
                 si = self.snap_i
                 self.snap_i = (si + 1) % self.n_snap

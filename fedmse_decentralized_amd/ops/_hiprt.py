@@ -70,6 +70,14 @@ def rt():
                 L.hipFree.restype = ctypes.c_int
                 L.hipMemcpy.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int]
                 L.hipMemcpy.restype = ctypes.c_int
+                L.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(vp), ctypes.c_uint]
+                L.hipEventCreateWithFlags.restype = ctypes.c_int
+                L.hipEventRecord.argtypes = [vp, vp]
+                L.hipEventRecord.restype = ctypes.c_int
+                L.hipStreamWaitEvent.argtypes = [vp, vp, ctypes.c_uint]
+                L.hipStreamWaitEvent.restype = ctypes.c_int
+                L.hipEventDestroy.argtypes = [vp]
+                L.hipEventDestroy.restype = ctypes.c_int
                 _lib = L
     return _lib
 
@@ -86,6 +94,50 @@ def device_sync() -> None:
     if rc != 0:
         raise RuntimeError(f"hipDeviceSynchronize failed ({rc})")
     SyncClock.tick()
+
+
+hipEventDisableTiming = 0x2
+hipEventDisableSystemFence = 0x20000000
+
+
+class DeviceEvent:
+    """A stream-order dependency between two streams of ONE device whose
+    consumers are kernels only.  Created with hipEventDisableSystemFence:
+    recording it skips the system-scope release (the L2 write-back that makes
+    device memory visible to the host and to other devices,
+    hip_runtime_api.h), which a kernel-to-kernel dependency on one device does
+    not need -- each kernel dispatch carries its own agent-scope release and
+    acquire, which is what orders two kernels of one stream across XCDs.  The
+    event is re-recorded every use (a wait enqueued after a record waits for
+    that record).  Never wait for it on the host, nor read mapped host memory
+    behind it: use a torch event for those."""
+
+    def __init__(self):
+        L = rt()
+        e = ctypes.c_void_p()
+        rc = L.hipEventCreateWithFlags(ctypes.byref(e), hipEventDisableTiming | hipEventDisableSystemFence)
+        if rc != 0:
+            raise RuntimeError(f"hipEventCreateWithFlags failed ({rc})")
+        self.handle = e
+
+    def record(self, stream: int) -> None:
+        rc = rt().hipEventRecord(self.handle, ctypes.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord failed ({rc})")
+
+    def wait(self, stream: int) -> None:
+        """Make ``stream`` wait (on the device) for the last record."""
+        rc = rt().hipStreamWaitEvent(ctypes.c_void_p(stream), self.handle, 0)
+        if rc != 0:
+            raise RuntimeError(f"hipStreamWaitEvent failed ({rc})")
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and _lib is not None:
+            try:
+                _lib.hipEventDestroy(h)
+            except Exception:   # interpreter shutdown
+                pass
 
 
 class SyncClock:

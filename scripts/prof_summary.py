@@ -4,7 +4,9 @@ Usage: python scripts/prof_summary.py gpurun_out/prof/run_results.db [--title T]
 
 Prints per-kernel totals (calls, total/avg/min/max us, share, VGPR/AGPR/SGPR,
 LDS, scratch) and, for the last bench round, the per-round kernel timeline
-(span from the first to the last kernel of one train->eval round).
+(span from the first to the last kernel of one train->eval round), and the
+median inter-round gap on the main stream (verification end -> next
+training start).
 """
 from __future__ import annotations
 
@@ -53,6 +55,19 @@ def summarize(db: str, title: str) -> str:
         for r in seg:
             out.append(f"| {(r[1] - t0) / 1000:.1f} | {r[3] / 1000:.1f} | {(r[1] - prev_end) / 1000:.1f} | `{_short(r[0])}` |")
             prev_end = r[2]
+    # the inter-round gap on the main stream: the end of each round's last
+    # protocol kernel (verification) to the start of the next training launch
+    gaps, last_v = [], None
+    for r in rows:
+        if "verify" in r[0] or "decide_adopt" in r[0]:
+            last_v = r[2]
+        elif "train_kernel" in r[0] and last_v is not None:
+            gaps.append((r[1] - last_v) / 1000.0)
+            last_v = None
+    if gaps:
+        g = sorted(gaps)
+        out += ["", f"inter-round gap (verification end -> next training start): median {g[len(g) // 2]:.1f} us, "
+                f"min {g[0]:.1f}, max {g[-1]:.1f} over {len(g)} rounds"]
     return "\n".join(out) + "\n"
 
 
