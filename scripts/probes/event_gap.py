@@ -10,7 +10,9 @@ write-back and invalidation, hip_runtime_api.h: hipEventDisableSystemFence);
 
 Each mode runs a loop of GPU-bound copies (~25 us each, the host stays ahead)
 with the named event traffic between them and reports the microseconds per
-iteration; the difference to ``none`` is what the event costs on the GPU.
+iteration; the difference to ``none`` is what the event costs on the GPU
+(``side-indep``: the side stream's kernel with no dependency at all, the
+floor of any cross-stream hand-off that needs no packet on the main stream).
 
     python scripts/probes/event_gap.py [--iters 400]
 """
@@ -67,6 +69,10 @@ def main():
             y.copy_(x)
             if mode == "none":
                 continue
+            if mode == "side-indep":   # side-stream work with no dependency on the main stream
+                with torch.cuda.stream(side):
+                    small.add_(1.0)
+                continue
             if mode.startswith("torch"):
                 e = torch.cuda.Event()
                 e.record(main_s)
@@ -82,7 +88,7 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / args.iters * 1e6
 
-    modes = ["none", "torch", "torch+side", "hip", "hip-device", "hip-nofence", "hip-device+side",
+    modes = ["none", "side-indep", "torch", "torch+side", "hip", "hip-device", "hip-nofence", "hip-device+side",
              "hip-nofence+side"]
     for m in modes:   # warm-up pass
         run(m)
