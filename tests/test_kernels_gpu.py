@@ -321,3 +321,31 @@ def test_forward_rows_independent_of_block_length():
         del os.environ["FEDMX_FWD_ROWS_PER_BLOCK"]
     for a, b in zip(sse_a, sse_b):
         assert torch.equal(a, b)
+
+
+def test_device_event_orders_two_streams():
+    """_hiprt.DeviceEvent (fence-less: the round's kernel-only stream
+    dependencies, engine/device_round.py): a side-stream copy waiting on it
+    sees what the main stream's kernels wrote before the record, every time
+    the one event is re-recorded."""
+    from fedmse_decentralized_amd.ops import _hiprt
+
+    ev = _hiprt.DeviceEvent()
+    main = torch.cuda.current_stream(DEV)
+    side = torch.cuda.Stream(DEV)
+    big = torch.empty(1 << 24, device=DEV)
+    src = torch.zeros(1 << 20, device=DEV)
+    outs = []
+    for it in range(20):
+        big.fill_(float(it))        # keeps the main stream busy (~64 MB write)
+        src.fill_(float(it + 1))    # the value the side stream must see
+        ev.record(main.cuda_stream)
+        out = torch.empty_like(src)
+        with torch.cuda.stream(side):
+            ev.wait(side.cuda_stream)
+            out.copy_(src)
+        outs.append(out)
+        main.wait_stream(side)      # the next fill_ of src comes after the copy
+    torch.cuda.synchronize()
+    for it, out in enumerate(outs):
+        assert bool((out == float(it + 1)).all()), it
