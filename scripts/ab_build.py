@@ -41,6 +41,9 @@ VARIANTS = {
     "av3nf": [("fedmx_train_hw.hip", "constexpr int ASYNC_VALID = 1;", "constexpr int ASYNC_VALID = 3;"),
               _mask("W4FLAG_ROLES", 2, 0)],
     "nf": [_mask("W4FLAG_ROLES", 2, 0)],
+    # the decision check two steps earlier (round 5 measured step 4 slower; the
+    # round-6 publication is faster: stamps put the decision ~3 steps after it)
+    "avc4": [_mask("AV_CHECK", 6, 4)],
     "stamps": [],   # (built with -DFEDMX_STAMPS=1 below)
 }
 FLAGS = {"stamps": ["-DFEDMX_STAMPS=1"]}
