@@ -44,9 +44,10 @@ VARIANTS = {
     # the decision check two steps earlier (round 5 measured step 4 slower; the
     # round-6 publication is faster: stamps put the decision ~3 steps after it)
     "avc4": [_mask("AV_CHECK", 6, 4)],
+    "avc4st": [_mask("AV_CHECK", 6, 4)],   # (stamped, below: the decision timeline at step 4)
     "stamps": [],   # (built with -DFEDMX_STAMPS=1 below)
 }
-FLAGS = {"stamps": ["-DFEDMX_STAMPS=1"]}
+FLAGS = {"stamps": ["-DFEDMX_STAMPS=1"], "avc4st": ["-DFEDMX_STAMPS=1"]}
 
 
 def build_variant(name: str) -> Path:
