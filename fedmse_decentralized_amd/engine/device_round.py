@@ -236,6 +236,20 @@ class DeviceRound:
             sse, drift, count = self.vsplit_scratch
             self.vsplit = _hip.VerifySplitArgs(sse=sse.data_ptr(), drift=drift.data_ptr(), count=count.data_ptr(),
                                                splits=max(1, min(64, -(-tiles // 8))), pad=0)
+        # side-stream hand-off (fedmx_protocol.hip vs_depart / side_wait_kernel):
+        # with split verification the round's evaluation waits on the
+        # verification kernel's own hand-off word, so the main stream carries
+        # no event between the verification and the next training launch
+        self.side_flag = None
+        if self.vsplit is not None and _hip.SIDE_FLAG:
+            khz = _hip.lib().fedmx_ipc_wall_khz()
+            status = _hip._hiprt.MappedBuffer(64)
+            view = status.view(0, np.int32, 1)
+            view[0] = 0
+            timeout_s = float(os.environ.get("FEDMX_SIDE_WAIT_TIMEOUT_S", "120"))
+            self.side_flag = dict(done=torch.zeros(2, dtype=i32, device=dev), status=status, view=view, seq=0,
+                                  ticks=int(timeout_s * 1e3 * (khz if khz > 0 else 100_000)))
+            self.vsplit.done = self.side_flag["done"].data_ptr()
         # the two per-round stream dependencies whose consumers are kernels only
         # (side -> main: the standardised vote data; main -> side: the round's
         # decisions and snapshots for the evaluation): fence-less device events
@@ -377,6 +391,9 @@ class DeviceRound:
         return c - self.start
 
     def _check_failed(self, rec: dict) -> None:
+        if self.side_flag is not None and int(self.side_flag["view"][0]) != 0:
+            raise RuntimeError(f"round {rec['round'] + 1}: the evaluation's wait for the verification kernel's "
+                               "hand-off ran out (FEDMX_SIDE_WAIT_TIMEOUT_S); rerun with FEDMX_SIDE_FLAG=0")
         if int(rec["report"][0]) == _hip.ELECT_TRAIN_FAILED:
             raise RuntimeError(f"round {rec['round'] + 1}: a training launch failed (a wave's bounded flag wait "
                                "or validator decision wait ran out); the device skipped that round's aggregation "
@@ -586,6 +603,9 @@ class DeviceRound:
                                     eval_params=eval_params.data_ptr(), best_stage=best_stage.data_ptr(),
                                     best=st.best.data_ptr(), latent=fed.dims.latent, hidden=fed.dims.hidden)
                 if self.vsplit is not None:
+                    if self.side_flag is not None:
+                        self.side_flag["seq"] += 1
+                        self.vsplit.seq = self.side_flag["seq"] & 0xFFFFFFFF
                     _hip.verify_split(v, self.vsplit, dev)
                 else:
                     _hip.verify_decide(v, dev)
@@ -599,14 +619,20 @@ class DeviceRound:
             nd = st.params.numel() // 2
             _hip.copy2_f64(eval_params.data_ptr(), st.params.data_ptr(), nd,
                            best_stage.data_ptr(), st.best.data_ptr(), nd, dev)
-        if self.dev_ev is not None:
+        side_flag = self.side_flag if (self.fused_verify and self.vsplit is not None) else None
+        if side_flag is not None:
+            ev_dec = None   # the verification kernel's hand-off word instead
+        elif self.dev_ev is not None:
             ev_dec = self.dev_ev[1]
             ev_dec.record(torch.cuda.current_stream(dev).cuda_stream)
         else:
             ev_dec = torch.cuda.Event()
             ev_dec.record()
         with tel.phase("eval"), _hip.on_stream(self.side):
-            if self.dev_ev is not None:
+            if side_flag is not None:
+                _hip.side_wait(side_flag["done"].data_ptr() + 4, side_flag["seq"], side_flag["status"].dev_ptr,
+                               side_flag["ticks"], self.side.cuda_stream)
+            elif self.dev_ev is not None:
                 ev_dec.wait(self.side.cuda_stream)
             else:
                 self.side.wait_event(ev_dec)

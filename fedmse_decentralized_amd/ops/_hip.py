@@ -130,13 +130,18 @@ class VerifyArgs(ctypes.Structure):
 class VerifySplitArgs(ctypes.Structure):
     """fedmx_protocol.hip verify_split_kernel: per-receiver scratch (SSE rows,
     drift granule, arrival counter) and the forward workgroups per receiver."""
-    _fields_ = [("sse", _vp), ("drift", _vp), ("count", _vp), ("splits", _i32), ("pad", _i32)]
+    _fields_ = [("sse", _vp), ("drift", _vp), ("count", _vp), ("splits", _i32), ("pad", _i32),
+                ("done", _vp), ("seq", ctypes.c_uint32), ("pad2", _i32)]
 
 
 # split verification (round 6): the verification forward over several
 # workgroups per receiver, a drift workgroup beside them, the last arriver
 # decides; "0" keeps the one-workgroup-per-receiver fused kernel
 VERIFY_SPLIT = os.environ.get("FEDMX_VERIFY_SPLIT", "1") != "0"
+# side-stream hand-off (round 6): with split verification, the round's
+# evaluation waits on the verification kernel's hand-off word (side_wait)
+# instead of an event recorded on the main stream; "0" keeps the event
+SIDE_FLAG = os.environ.get("FEDMX_SIDE_FLAG", "1") != "0"
 
 
 def lib():
@@ -169,6 +174,7 @@ def lib():
                 "fedmx_decide_adopt": [ctypes.POINTER(DecideArgs), vp],
                 "fedmx_verify_decide": [ctypes.POINTER(VerifyArgs), vp],
                 "fedmx_verify_split": [ctypes.POINTER(VerifyArgs), ctypes.POINTER(VerifySplitArgs), vp],
+                "fedmx_side_wait": [vp, ctypes.c_uint32, vp, ctypes.c_longlong, vp],
                 "fedmx_copy_f64": [vp, vp, i32, vp],
                 "fedmx_copy2_f64": [vp, vp, i32, vp, vp, i32, vp],
                 "fedmx_copy_rows": [vp, i32, vp, vp, i32, vp, i32, i32, vp],
@@ -665,6 +671,16 @@ def verify_split(args: VerifyArgs, sargs: VerifySplitArgs, device):
     forward spread over ``sargs.splits`` workgroups and its drift over one
     more (modes 0 / 1 / 3; the thesis rule keeps verify_decide)."""
     _check(lib().fedmx_verify_split(ctypes.byref(args), ctypes.byref(sargs), _stream(device)), "fedmx_verify_split")
+
+
+def side_wait(word_ptr: int, seq: int, status_ptr: int, timeout_ticks: int, stream: int):
+    """Enqueue on ``stream`` a one-lane wait until the 32-bit word at
+    ``word_ptr`` reaches ``seq`` (verify_split_kernel's hand-off word);
+    past ``timeout_ticks`` (wall_clock64 ticks) it sets the int32 at
+    ``status_ptr`` (host-visible) and lets the stream go on."""
+    _check(lib().fedmx_side_wait(ctypes.c_void_p(word_ptr), ctypes.c_uint32(seq & 0xFFFFFFFF),
+                                 ctypes.c_void_p(status_ptr), ctypes.c_longlong(timeout_ticks),
+                                 ctypes.c_void_p(stream)), "fedmx_side_wait")
 
 
 def copy_f64(dst_ptr: int, src_ptr: int, n: int, device):

@@ -745,13 +745,45 @@ struct VerifySplitArgs {
   uint32_t* count;            // [n_local] arrivals; zero between launches (zeroed once; the last arriver resets)
   int32_t splits;             // forward workgroups per receiver (>= 1)
   int32_t pad;
+  uint32_t* done;             // or null: [2] = {departed workgroups (zero between launches), hand-off word}
+  uint32_t seq;               // written to done[1] by the launch's last departing workgroup
+  int32_t pad2;
 };
-static_assert(sizeof(VerifySplitArgs) == 32, "VerifySplitArgs layout is shared with Python");
+static_assert(sizeof(VerifySplitArgs) == 48, "VerifySplitArgs layout is shared with Python");
+
+// The side-stream hand-off (round 6): the round's evaluation on the side
+// stream reads what this kernel writes for it -- the evaluation snapshot
+// (eval_params), the artefact snapshot (best_stage) and the rejection counts
+// (rej_out) -- and nothing else of it.  Those are written with sc1 stores;
+// every workgroup drains them, passes the workgroup barrier and adds 1 to
+// done[0] (one lane, agent scope); the last one (its add returned the grid
+// size - 1) resets done[0] and stores `seq` into done[1], on which
+// side_wait_kernel polls (cdna_hip_programming.md §6 Guideline 16 R1, the
+// hand-off the verification's own last-arriver step uses).  The evaluation
+// kernels behind side_wait_kernel start with their dispatch's acquire, so no
+// stale L2 line of the snapshots survives into them.  The round's main
+// stream then needs no event between this kernel and the next training
+// launch (engine/device_round.py; profiles/r6_device_events_ab.md: the
+// event's marker packet costs the main stream ~2.6 us per round).
+__device__ __forceinline__ void vs_depart(const VerifySplitArgs& S) {
+  typedef __attribute__((address_space(1))) uint32_t gu32;
+  if (S.done == nullptr) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add((gu32*)S.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __hip_atomic_store((gu32*)S.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu32*)(S.done + 1), S.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t vs_rsrc(float* p, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, bytes, 0x00020000);
 }
+constexpr int SC1 = 16;   // buffer instruction cache-policy bits: sc1
 
 template <bool CP, bool REL>
 __global__ __launch_bounds__(512) void verify_split_kernel(const VerifyArgs V, const VerifySplitArgs S) {
@@ -774,11 +806,14 @@ __global__ __launch_bounds__(512) void verify_split_kernel(const VerifyArgs V, c
   if ((int)blockIdx.x >= nver) {
     // the artefact snapshot best -> best_stage (as in verify_decide_kernel)
     const int cl2 = blockIdx.x - nver;
-    if (cl2 >= A.n_local) return;
-    const size_t o2 = (size_t)cl2 * A.P;
-    const f32x4* b = reinterpret_cast<const f32x4*>(V.best + o2);
-    f32x4* bs = reinterpret_cast<f32x4*>(V.best_stage + o2);
-    for (int i = threadIdx.x; i < A.P / 4; i += blockDim.x) bs[i] = b[i];
+    if (cl2 < A.n_local) {
+      const size_t o2 = (size_t)cl2 * A.P;
+      const f32x4* b = reinterpret_cast<const f32x4*>(V.best + o2);
+      const __amdgpu_buffer_rsrc_t bs = vs_rsrc(V.best_stage + o2, 4 * A.P);   // (side-stream input)
+      for (int i = threadIdx.x; i < A.P / 4; i += blockDim.x)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, b[i]), bs, 16 * i, 0, SC1);
+    }
+    vs_depart(S);
     return;
   }
   const int cl = blockIdx.x / per, role = blockIdx.x % per;
@@ -893,7 +928,10 @@ __global__ __launch_bounds__(512) void verify_split_kernel(const VerifyArgs V, c
     if (s_last) __hip_atomic_store((gu32*)(S.count + cl), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  if (!s_last) return;
+  if (!s_last) {
+    vs_depart(S);
+    return;
+  }
   bool ok = false, load = false;
   if (a >= 0 && A.mode == 1) {
     load = ok = true;   // centralised push: every hosted client loads and re-anchors
@@ -938,7 +976,8 @@ __global__ __launch_bounds__(512) void verify_split_kernel(const VerifyArgs V, c
       A.hist_perf[cl] = perf;
       const int rj = okk ? 0 : A.rejected[cl] + 1;
       A.rejected[cl] = rj;
-      A.rej_out[c] = (double)rj;
+      __hip_atomic_store((gu64*)(A.rej_out + c), __builtin_bit_cast(unsigned long long, (double)rj),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (side-stream input)
       s_ok = okk;
     }
     __syncthreads();
@@ -950,7 +989,7 @@ __global__ __launch_bounds__(512) void verify_split_kernel(const VerifyArgs V, c
   const int n4 = A.P / 4;
   const f32x4* src = reinterpret_cast<const f32x4*>(A.agg);
   f32x4* prm = reinterpret_cast<f32x4*>(A.params + off);
-  f32x4* evp = reinterpret_cast<f32x4*>(V.eval_params + off);
+  const __amdgpu_buffer_rsrc_t evp = vs_rsrc(V.eval_params + off, 4 * A.P);   // (side-stream input)
   constexpr int UA = (P_PAD / 4 + 511) / 512;
   f32x4 v[UA], pv[UA];
 #pragma unroll
@@ -970,8 +1009,28 @@ __global__ __launch_bounds__(512) void verify_split_kernel(const VerifyArgs V, c
         if (ok) reinterpret_cast<f32x4*>(A.anchor + off)[i] = v[u];
       }
       if (receiver) reinterpret_cast<f32x4*>(A.hist + off)[i] = v[u];
-      evp[i] = pv[u];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, pv[u]), evp, 16 * i, 0, SC1);
     }
+  }
+  vs_depart(S);
+}
+
+// The side stream's wait for the verification's hand-off word (vs_depart):
+// one lane polls done[1] until it reaches `seq` (bounded: past timeout_ticks
+// it sets the host-visible status word and exits, and the host raises when
+// it collects the round).  Nothing else -- the evaluation kernels behind it
+// acquire at their own dispatch.
+__global__ __launch_bounds__(64) void side_wait_kernel(uint32_t* word, uint32_t seq, int* status,
+                                                       long long timeout_ticks) {
+  typedef __attribute__((address_space(1))) uint32_t gu32;
+  if (threadIdx.x != 0) return;
+  const long long t0 = (long long)wall_clock64();
+  while ((int)(__hip_atomic_load((gu32*)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0) {
+    if ((long long)wall_clock64() - t0 > timeout_ticks) {
+      if (status) __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
   }
 }
 
@@ -1069,6 +1128,12 @@ int fedmx_verify_split(const void* args, const void* sargs, hipStream_t stream) 
   } else {
     hipLaunchKernelGGL((fedmx::verify_split_kernel<false, false>), grid, dim3(512), 0, stream, V, S);
   }
+  return (int)hipGetLastError();
+}
+
+int fedmx_side_wait(void* word, uint32_t seq, void* status, long long timeout_ticks, hipStream_t stream) {
+  hipLaunchKernelGGL(fedmx::side_wait_kernel, dim3(1), dim3(64), 0, stream, reinterpret_cast<uint32_t*>(word), seq,
+                     reinterpret_cast<int*>(status), timeout_ticks);
   return (int)hipGetLastError();
 }
 

@@ -349,3 +349,31 @@ def test_device_event_orders_two_streams():
     torch.cuda.synchronize()
     for it, out in enumerate(outs):
         assert bool((out == float(it + 1)).all()), it
+
+
+def test_side_wait_returns_on_the_word_and_times_out_without_it():
+    """side_wait_kernel (the round's evaluation waiting on verify_split's
+    hand-off word, engine/device_round.py): it returns once the word reaches
+    the sequence number (wrap-safe), and without the word it gives up after
+    its timeout and sets the host-visible status word."""
+    from fedmse_decentralized_amd.ops import _hiprt
+
+    khz = _hip.lib().fedmx_ipc_wall_khz()
+    ticks_per_ms = khz if khz > 0 else 100_000
+    status = _hiprt.MappedBuffer(64)
+    view = status.view(0, np.int32, 1)
+    word = torch.zeros(2, dtype=torch.int32, device=DEV)
+    side = torch.cuda.Stream(DEV)
+    for stored, seq in ((7, 7), (9, 7), (-2, 0xFFFFFFFE), (1, 0xFFFFFFFF)):   # reached (the last two across the wrap)
+        view[0] = 0
+        word[1] = stored
+        torch.cuda.synchronize()
+        _hip.side_wait(word.data_ptr() + 4, seq, status.dev_ptr, 1000 * ticks_per_ms, side.cuda_stream)
+        side.synchronize()
+        assert int(view[0]) == 0, (stored, seq)
+    view[0] = 0
+    word[1] = 5
+    torch.cuda.synchronize()
+    _hip.side_wait(word.data_ptr() + 4, 6, status.dev_ptr, 20 * ticks_per_ms, side.cuda_stream)   # never reached
+    side.synchronize()
+    assert int(view[0]) == 1
