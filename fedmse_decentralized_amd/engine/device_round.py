@@ -57,6 +57,7 @@ from ..ops import _hip
 # fence-less device events for the kernel-to-kernel stream dependencies
 # ("0": torch events, which record with a system-scope fence)
 _DEVICE_EVENTS = os.environ.get("FEDMX_DEVICE_EVENTS", "1") != "0"
+_SIDE_FLAG_KEEPALIVE: list = []   # (hand-off word, status buffer) of every DeviceRound (a few bytes each)
 
 log = logging.getLogger("fedmx")
 
@@ -250,6 +251,11 @@ class DeviceRound:
             self.side_flag = dict(done=torch.zeros(2, dtype=i32, device=dev), status=status, view=view, seq=0,
                                   ticks=int(timeout_s * 1e3 * (khz if khz > 0 else 100_000)))
             self.vsplit.done = self.side_flag["done"].data_ptr()
+            # both streams use these through raw pointers (the verification
+            # kernel on the main stream writes the word, the side stream's
+            # wait reads it and may write the status): never released, so no
+            # later allocation can reuse them under a wait still in flight
+            _SIDE_FLAG_KEEPALIVE.append((self.side_flag["done"], status))
         # the two per-round stream dependencies whose consumers are kernels only
         # (side -> main: the standardised vote data; main -> side: the round's
         # decisions and snapshots for the evaluation): fence-less device events
