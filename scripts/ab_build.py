@@ -46,8 +46,17 @@ VARIANTS = {
     "avc4": [_mask("AV_CHECK", 6, 4)],
     "avc4st": [_mask("AV_CHECK", 6, 4)],   # (stamped, below: the decision timeline at step 4)
     "stamps": [],   # (built with -DFEDMX_STAMPS=1 below)
+    # round-6 compiler-scheduler sweep: the production sources, other
+    # machine-scheduler settings (no numerics change: bit-identical results)
+    "s_ilp": [], "s_iterilp": [], "s_nounclust": [], "s_trackers": [], "s_bias0": [], "s_relaxed": [],
 }
-FLAGS = {"stamps": ["-DFEDMX_STAMPS=1"], "avc4st": ["-DFEDMX_STAMPS=1"]}
+FLAGS = {"stamps": ["-DFEDMX_STAMPS=1"], "avc4st": ["-DFEDMX_STAMPS=1"],
+         "s_ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+         "s_iterilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+         "s_nounclust": ["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"],
+         "s_trackers": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
+         "s_bias0": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],
+         "s_relaxed": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"]}
 
 
 def build_variant(name: str) -> Path:
