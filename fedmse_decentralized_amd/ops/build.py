@@ -94,6 +94,9 @@ def _stamp(target: Path, digest: str) -> None:
 
 
 def _run(cmd, cwd=None):
+    """Run one command (a list of arguments) or several in order (a list of such lists)."""
+    if cmd and isinstance(cmd[0], (list, tuple)):
+        return "".join(_run(c, cwd) for c in cmd)
     r = subprocess.run(cmd, cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         raise RuntimeError("build failed: " + " ".join(map(str, cmd)) + "\n" + r.stdout)
@@ -118,7 +121,11 @@ def _build(target: Path, digest: str, cmd_for, force: bool, verbose: bool) -> Pa
             BUILD_STATUS[target] = ("reused", digest)
             return target
         tmp = target.with_name(f"{target.name}.{os.getpid()}.tmp")
-        out = _run(cmd_for(tmp))
+        try:
+            out = _run(cmd_for(tmp))
+        finally:
+            for o in target.parent.glob(f"{tmp.name}.*.o"):   # per-source objects (hip_link_commands)
+                o.unlink()
         os.replace(tmp, target)
         _stamp(target, digest)
     BUILD_STATUS[target] = ("compiled", digest)
@@ -154,10 +161,36 @@ def build_hip(force: bool = False, verbose: bool = False, extra_flags=(), target
     # optimizer tail: -3.3% launch time measured)
     base = _hip_flags(extra_flags)
     flags = [*base[:3], "-fPIC", "-shared", *base[3:]]
-    digest = content_hash([compiler_identity(hipcc_path()), *flags, *(p.name for p in srcs)], srcs + _headers())
-    return _build(target, digest,
-                  lambda tmp: [hipcc_path(), *flags, f"-I{CSRC / 'hip'}", *map(str, srcs), "-o", str(tmp)],
-                  force, verbose)
+    digest = content_hash([compiler_identity(hipcc_path()), *flags, *(p.name for p in srcs),
+                           *(f"{k}:{' '.join(v)}" for k, v in sorted(SOURCE_FLAGS.items()))], srcs + _headers())
+    return _build(target, digest, lambda tmp: hip_link_commands(srcs, flags, CSRC / "hip", tmp), force, verbose)
+
+
+# Per-source flags, added to the library's for that translation unit only: the
+# FedProx instantiation of the helper-wave training kernel compiles with the
+# machine scheduler's memory-operation clustering off (966 -> 939 us per
+# launch; the same flag costs the other instantiations 1-2.5 %,
+# profiles/r6_fedprox_nocluster.md)
+SOURCE_FLAGS = {"fedmx_train_hw_prox.hip": ["-mllvm", "-misched-cluster=false"]}
+
+
+def hip_link_commands(srcs, flags, include_dir: Path, out: Path) -> list:
+    """The commands that build one kernel library: every source listed in
+    SOURCE_FLAGS compiled to an object of its own (``<out>.<stem>.o``), then
+    one hipcc line over the other sources and those objects."""
+    cmds, objs, rest = [], [], []
+    obj_flags = [f for f in flags if f != "-shared"]
+    for p in srcs:
+        extra = SOURCE_FLAGS.get(Path(p).name)
+        if extra:
+            o = Path(out).with_name(f"{Path(out).name}.{Path(p).stem}.o")
+            cmds.append([hipcc_path(), *obj_flags, *extra, f"-I{include_dir}", "-c", str(p), "-o", str(o)])
+            objs.append(o)
+        else:
+            rest.append(p)
+    # (objects before the sources: hipcc marks every source `-x hip`, which would also apply to a later object)
+    cmds.append([hipcc_path(), *flags, f"-I{include_dir}", *map(str, objs), *map(str, rest), "-o", str(out)])
+    return cmds
 
 
 def _hip_flags(extra_flags=()):
@@ -209,6 +242,7 @@ def train_resource_report(extra_flags=()) -> str:
              "_ZN5fedmx2hw15train_kernel_hwILb0ELb1EEEvNS_9TrainArgsE": "plain, batch > 12",
              "_ZN5fedmx2hw15train_kernel_hwILb1ELb1EEEvNS_9TrainArgsE": "FedProx, batch > 12"}
     res = kernel_resources("fedmx_train_hw.hip", extra_flags)
+    res.update(kernel_resources("fedmx_train_hw_prox.hip", [*extra_flags, *SOURCE_FLAGS["fedmx_train_hw_prox.hip"]]))
     rows = ["instantiation            VGPR  VGPR-spill  SGPR-spill  scratch B/lane  LDS B"]
     for k, label in names.items():
         r = res.get(k, {})

@@ -1655,6 +1655,17 @@ __global__ __launch_bounds__(512, 1) void train_kernel_hw(const TrainArgs A) {
 }  // namespace hw
 }  // namespace fedmx
 
+#ifdef FEDMX_HW_PROX_TU
+// fedmx_train_hw_prox.hip: this TU holds the FedProx instantiation for batch
+// <= 12 only, compiled with its own scheduler flags (ops/build.py SOURCE_FLAGS)
+extern "C" int fedmx_train_hw_prox_launch(const void* args, int grid, hipStream_t stream) {
+  const fedmx::TrainArgs A = *reinterpret_cast<const fedmx::TrainArgs*>(args);
+  hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true, false>), dim3(grid), dim3(512), 0, stream, A);
+  return (int)hipGetLastError();
+}
+#else
+extern "C" int fedmx_train_hw_prox_launch(const void* args, int grid, hipStream_t stream);
+
 extern "C" {
 
 static int g_last_grid = 0;   // workgroups of the last helper-wave launch (tests: 2k = validators ran)
@@ -1694,7 +1705,7 @@ int fedmx_train_hw(const void* args, int k, hipStream_t stream) {
     if (multi)
       hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true, true>), dim3(grid), dim3(512), 0, stream, A);
     else
-      hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<true, false>), dim3(grid), dim3(512), 0, stream, A);
+      return fedmx_train_hw_prox_launch(&A, grid, stream);   // (fedmx_train_hw_prox.hip)
   } else {
     if (multi)
       hipLaunchKernelGGL((fedmx::hw::train_kernel_hw<false, true>), dim3(grid), dim3(512), 0, stream, A);
@@ -1708,3 +1719,4 @@ int fedmx_train_hw(const void* args, int k, hipStream_t stream) {
 int fedmx_train_av_slot(void) { return fedmx::hw::AV_SLOT; }
 
 }  // extern "C"
+#endif  // FEDMX_HW_PROX_TU

@@ -49,6 +49,9 @@ VARIANTS = {
     # round-6 compiler-scheduler sweep: the production sources, other
     # machine-scheduler settings (no numerics change: bit-identical results)
     "s_ilp": [], "s_iterilp": [], "s_nounclust": [], "s_trackers": [], "s_bias0": [], "s_relaxed": [],
+    "s_agpr": [], "s_o2": [], "s_exact": [], "s_nocluster": [], "s_bias100": [],
+    # FedProx with asynchronous validation, memory clustering off
+    "av3_nocluster": [("fedmx_train_hw.hip", "constexpr int ASYNC_VALID = 1;", "constexpr int ASYNC_VALID = 3;")],
 }
 FLAGS = {"stamps": ["-DFEDMX_STAMPS=1"], "avc4st": ["-DFEDMX_STAMPS=1"],
          "s_ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
@@ -56,7 +59,13 @@ FLAGS = {"stamps": ["-DFEDMX_STAMPS=1"], "avc4st": ["-DFEDMX_STAMPS=1"],
          "s_nounclust": ["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"],
          "s_trackers": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
          "s_bias0": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],
-         "s_relaxed": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"]}
+         "s_relaxed": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"],
+         "s_agpr": ["-mllvm", "-amdgpu-mfma-vgpr-form=0"],   # (the last -mllvm setting wins)
+         "s_o2": ["-O2"],
+         "s_exact": ["-mllvm", "-amdgpu-igrouplp-exact-solver"],
+         "s_nocluster": ["-mllvm", "-misched-cluster=false"],
+         "s_bias100": ["-mllvm", "-amdgpu-schedule-metric-bias=100"],
+         "av3_nocluster": ["-mllvm", "-misched-cluster=false"]}
 
 
 def build_variant(name: str) -> Path:
@@ -73,11 +82,15 @@ def build_variant(name: str) -> Path:
             p.write_text(text.replace(old, new))
         target = build.LIBDIR / f"libfedmx_hip_{name}.so"
         base = build._hip_flags(FLAGS.get(name, []))
-        cmd = [build.hipcc_path(), *base[:3], "-fPIC", "-shared", *base[3:], f"-I{dst}",
-               *map(str, sorted(dst.glob("*.hip"))), "-o", str(target)]
-        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
-        if r.returncode != 0:
-            raise SystemExit(f"variant {name} failed:\n{r.stdout[-3000:]}")
+        flags = [*base[:3], "-fPIC", "-shared", *base[3:]]
+        # the library's own per-source flags too (build.SOURCE_FLAGS), so a
+        # variant differs from production only by its substitutions / FLAGS
+        for cmd in build.hip_link_commands(sorted(dst.glob("*.hip")), flags, dst, target):
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+            if r.returncode != 0:
+                raise SystemExit(f"variant {name} failed:\n{r.stdout[-3000:]}")
+        for o in target.parent.glob(f"{target.name}.*.o"):
+            o.unlink()
     return target
 
 

@@ -63,8 +63,14 @@ def test_compiler_identity_is_part_of_the_build_hash(tmp_path, monkeypatch):
     lib = tmp_path / "libfake.so"
     calls = []
     monkeypatch.setattr(build, "LIBDIR", tmp_path)
-    monkeypatch.setattr(build, "_run", lambda cmd, cwd=None: (calls.append(cmd), open(cmd[-1], "wb").close())[1]
-                        or "")
+    def fake_run(cmd, cwd=None):
+        # one build = one call; a library with per-source objects (build.SOURCE_FLAGS)
+        # is several commands, the last one writing the library
+        calls.append(cmd)
+        last = cmd[-1] if isinstance(cmd[-1], (list, tuple)) else cmd
+        open(last[-1], "wb").close()
+        return ""
+    monkeypatch.setattr(build, "_run", fake_run)
     build.build_hip(target=lib)
     assert build.BUILD_STATUS[lib][0] == "compiled" and len(calls) == 1
     build.build_hip(target=lib)
