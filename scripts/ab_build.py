@@ -50,6 +50,8 @@ VARIANTS = {
     # machine-scheduler settings (no numerics change: bit-identical results)
     "s_ilp": [], "s_iterilp": [], "s_nounclust": [], "s_trackers": [], "s_bias0": [], "s_relaxed": [],
     "s_agpr": [], "s_o2": [], "s_exact": [], "s_nocluster": [], "s_bias100": [],
+    "m_pre_td": [], "m_pre_bu": [], "m_post_td": [], "m_post_bu": [], "m_nopost": [], "m_nocyclic": [],
+    "m_norp": [],
     # FedProx with asynchronous validation, memory clustering off
     "av3_nocluster": [("fedmx_train_hw.hip", "constexpr int ASYNC_VALID = 1;", "constexpr int ASYNC_VALID = 3;")],
 }
@@ -65,7 +67,14 @@ FLAGS = {"stamps": ["-DFEDMX_STAMPS=1"], "avc4st": ["-DFEDMX_STAMPS=1"],
          "s_exact": ["-mllvm", "-amdgpu-igrouplp-exact-solver"],
          "s_nocluster": ["-mllvm", "-misched-cluster=false"],
          "s_bias100": ["-mllvm", "-amdgpu-schedule-metric-bias=100"],
-         "av3_nocluster": ["-mllvm", "-misched-cluster=false"]}
+         "av3_nocluster": ["-mllvm", "-misched-cluster=false"],
+         "m_pre_td": ["-mllvm", "-misched-prera-direction=topdown"],
+         "m_pre_bu": ["-mllvm", "-misched-prera-direction=bottomup"],
+         "m_post_td": ["-mllvm", "-misched-postra-direction=topdown"],
+         "m_post_bu": ["-mllvm", "-misched-postra-direction=bottomup"],
+         "m_nopost": ["-mllvm", "-enable-post-misched=false"],
+         "m_nocyclic": ["-mllvm", "-misched-cyclicpath=false"],
+         "m_norp": ["-mllvm", "-misched-regpressure=false"]}
 
 
 def build_variant(name: str) -> Path:
