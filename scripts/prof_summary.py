@@ -21,6 +21,9 @@ def _short(name: str, n: int = 70) -> str:
     return s if len(s) <= n else s[: n - 3] + "..."
 
 
+POLLING = ("side_wait_kernel",)
+
+
 def summarize(db: str, title: str) -> str:
     c = sqlite3.connect(db)
     rows = c.execute("select name, start, end, duration, grid_x, grid_y, workgroup_x, lds_size, scratch_size, "
@@ -34,13 +37,17 @@ def summarize(db: str, title: str) -> str:
         a["tot"] += d
         a["mn"] = min(a["mn"], d)
         a["mx"] = max(a["mx"], d)
-    total = sum(a["tot"] for a in agg.values()) or 1.0
+    # polling kernels (a lane that sleeps between loads while the round runs,
+    # e.g. side_wait_kernel) are not GPU work: kept out of the % column
+    polling = [n for n in agg if any(p in n for p in POLLING)]
+    total = sum(a["tot"] for n, a in agg.items() if n not in polling) or 1.0
     out += ["| kernel | calls | total us | avg us | min us | max us | % | grid | VGPR/AGPR/SGPR | LDS B | scratch B |",
             "|---|---|---|---|---|---|---|---|---|---|---|"]
     for name, a in sorted(agg.items(), key=lambda kv: -kv[1]["tot"]):
         gx, gy, wg, lds, scr, vg, ag, sg = a["meta"]
+        share = "polling" if name in polling else f"{100 * a['tot'] / total:.1f}"
         out.append(f"| `{_short(name)}` | {a['n']} | {a['tot']:.1f} | {a['tot'] / a['n']:.1f} | {a['mn']:.1f} | "
-                   f"{a['mx']:.1f} | {100 * a['tot'] / total:.1f} | {gx // max(wg, 1)}x{gy} | {vg}/{ag}/{sg} | {lds} | {scr} |")
+                   f"{a['mx']:.1f} | {share} | {gx // max(wg, 1)}x{gy} | {vg}/{ag}/{sg} | {lds} | {scr} |")
     # last round: from the last train_kernel launch to the end of the next auc kernel
     starts = [i for i, r in enumerate(rows) if "train_kernel" in r[0]]
     if starts:
