@@ -41,7 +41,8 @@ def summarize(db: str, title: str) -> str:
     # e.g. side_wait_kernel) are not GPU work: kept out of the % column
     polling = [n for n in agg if any(p in n for p in POLLING)]
     total = sum(a["tot"] for n, a in agg.items() if n not in polling) or 1.0
-    out += ["| kernel | calls | total us | avg us | min us | max us | % | grid | VGPR/AGPR/SGPR | LDS B | scratch B |",
+    out += ["| kernel | calls | total us | avg us | min us | max us | % (polling kernels excluded) | grid | VGPR/AGPR/SGPR "
+            "| LDS B | scratch B |",
             "|---|---|---|---|---|---|---|---|---|---|---|"]
     for name, a in sorted(agg.items(), key=lambda kv: -kv[1]["tot"]):
         gx, gy, wg, lds, scr, vg, ag, sg = a["meta"]
