@@ -14,6 +14,9 @@
 //                       parity test
 //   FEDMX_STAMPS=1      in-kernel s_memtime phase stamps (libfedmx_hip_stamps.so,
 //                       scripts/train_stamps.py)
+// (FEDMX_HW_PROX_TU is no variant: it selects which part of
+// fedmx_train_hw.hip a translation unit holds -- fedmx_train_hw_prox.hip,
+// the FedProx instantiation under its own compiler flags)
 #ifndef FEDMX_EXACT_ADAM
 #define FEDMX_EXACT_ADAM 0
 #endif
