@@ -84,6 +84,9 @@ def main():
     # batch 64 (the thesis's GPU runs): helper-wave kernel (16-row chunks) vs the 4-wave kernel
     hp64 = TrainHParams(epochs=args.epochs, batch_size=64, lr=1e-3, shrink_lambda=5.0, patience=10 ** 6)
     out["train_launch_b64_us"] = timeit(lambda: eng.train_async(sel, hp64), reps=args.reps)[0]
+    hp64p = TrainHParams(epochs=args.epochs, batch_size=64, lr=1e-3, shrink_lambda=5.0, fedprox_mu=0.001,
+                         patience=10 ** 6)
+    out["train_launch_b64_fedprox_us"] = timeit(lambda: eng.train_async(sel, hp64p), reps=args.reps)[0]
     prev, _hip.TRAIN_HELPER = _hip.TRAIN_HELPER, False
     out["train_launch_b64_4wave_us"] = timeit(lambda: eng.train_async(sel, hp64), reps=args.reps)[0]
     _hip.TRAIN_HELPER = prev
